@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s (+ Msamples/s) of the MI355X per-pixel integration path.
+
+Workload (BASELINE.json configs[2], the config the north-star target is quoted on):
+bunny.sp at 1920x1080, 256 samples per pixel, DirectLighting (the reference's default integrator
+for a scene file that names none: main.cpp:387-392), SAH BVH.  One step = one full frame.
+With --gpus N > 1 (one process per GPU via torch.distributed.run) the frame's 8x8 tiles are
+sharded across ranks (TileScheduler order, interleaved) and gathered to rank 0 with a single
+RCCL gather at frame end: strong scaling (fixed total work).
+
+Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects; see DESIGN.md §Measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+MT_BYTES_PER_DRAW = 24.0  # 8 B draw read + (2496 B twist read + 2496 B write) / 312
+PIXEL_BYTES = 12.0  # one float3 radiance store per pixel
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--integrator", default="direct_lighting")
+    ap.add_argument("--bvh", type=int, default=0, help="0 = SAH, 1 = reference median split")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+        local = 0
+
+    import simplepath_amd as sp
+    from simplepath_amd import scenes
+
+    scene_dir = os.path.join(tempfile.gettempdir(), f"sp_bench_{os.getuid()}")
+    if rank == 0:
+        path = scenes.write_bunny_scene(scene_dir)
+    if dist is not None:
+        dist.barrier()
+    path = os.path.join(scene_dir, "bunny.sp")
+    scene = sp.Scene.from_file(path)
+    scene.set_resolution(args.width, args.height)
+    scene.upload(device=local, bvh_mode=args.bvh)
+    integ = sp.string_to_integrator_type(args.integrator)
+
+    sched = sp.ColumnMajorTileScheduler(args.width, args.height)
+    n_tiles = sched.get_num_tiles()
+    my_tiles = sched.shard(rank, world)
+    per_rank = (n_tiles + world - 1) // world
+    out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
+    gathered = None
+    if dist is not None and rank == 0:
+        gathered = [torch.zeros_like(out) for _ in range(world)]
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        st = sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream)
+        if dist is not None:
+            dist.gather(out, gathered if rank == 0 else None, dst=0)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        stats.append(step())
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    rays = sum(s.rays for s in stats)
+    samples = sum(s.samples for s in stats)
+    draws = sum(s.rng_draws for s in stats)
+    kernel_ms = sum(s.kernel_ms for s in stats) / max(1, len(stats))
+    if dist is not None:
+        t = torch.tensor([elapsed, float(rays), float(samples), float(draws)], dtype=torch.float64, device=f"cuda:{local}")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0])
+        rays, samples, draws = float(t[1]), float(t[2]), float(t[3])
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    mrays = rays / elapsed / 1e6
+    msamples = samples / elapsed / 1e6
+    # ---- roofline of the dominant kernel (sp_render_kernel), per launch on this rank
+    per_launch_draws = sum(s.rng_draws for s in stats) / len(stats)
+    per_launch_pixels = min(len(my_tiles) * 64, args.width * args.height)
+    alg_bytes = per_launch_draws * MT_BYTES_PER_DRAW + per_launch_pixels * PIXEL_BYTES
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as fh:
+                tj = json.load(fh)
+            if tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": "sp_render_kernel", "kernel_ms": round(kernel_ms, 3),
+                "alg_bytes_per_launch": alg_bytes}
+
+    cpu = None
+    parity = None
+    if not args.no_cpu:
+        cpu, parity = cpu_baseline(scene, integ, args, out if world == 1 else None, my_tiles)
+
+    line = {
+        "metric": "Mrays/sec (+ Msamples/sec) at fixed spp; per-pixel L2 vs CPU ref",
+        "value": round(mrays, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (bunny-like PLY generated in-process; scene parameters of scenes/bunny.sp)",
+        "config": {"workload": f"bunny.sp {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
+                   "width": args.width, "height": args.height, "spp": args.spp, "integrator": args.integrator,
+                   "bvh": "sah" if args.bvh == 0 else "reference", "tiles": int(n_tiles),
+                   "parallelism": f"tiles{world}"},
+        "msamples_per_s": round(msamples, 3),
+        "rays_per_step": rays / args.steps,
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(scene, integ, args, gpu_out, my_tiles):
+    """Time the CPU oracle (glibc = reference semantics, "port") on a bounded sample of the same
+    frame: whole 8x8 tiles spread over the image, same spp and integrator, until about
+    --cpu-seconds of work; also compares those tiles with the GPU frame (rel L2, bit-exact share)."""
+    import simplepath_amd as sp
+    from tests import _oracle
+
+    n_tiles = sp.TileScheduler(args.width, args.height).get_num_tiles()
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    rng = np.random.default_rng(1234)
+    order = rng.permutation(n_tiles).astype(np.int32)
+    done, t_used, rays, samples = [], 0.0, 0, 0
+    chunk = threads
+    tiles_out = []
+    while t_used < args.cpu_seconds and len(done) < n_tiles:
+        ids = order[len(done):len(done) + chunk]
+        t0 = time.perf_counter()
+        out, st = _oracle.render(scene, integ, args.spp, ids, threads=threads, variant="glibc")
+        dt = time.perf_counter() - t0
+        t_used += dt
+        rays += st["rays"]
+        samples += st["samples"]
+        done.extend(ids.tolist())
+        tiles_out.append(out)
+        if dt < args.cpu_seconds / 8:
+            chunk *= 2
+    cpu = {"value": round(rays / t_used / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "sample": f"{len(done)} random 8x8 tiles of the same frame @ {args.spp} spp ({samples} samples, "
+                     f"{t_used:.1f} s, oracle/liboracle_glibc.so)",
+           "msamples_per_s": round(samples / t_used / 1e6, 5)}
+    parity = None
+    if gpu_out is not None:
+        ref = np.concatenate(tiles_out, axis=0)
+        gpu = gpu_out.cpu().numpy()
+        pos = {int(t): i for i, t in enumerate(my_tiles)}
+        g = np.stack([gpu[pos[t]] for t in done])
+        diff = np.linalg.norm((g - ref).ravel())
+        norm = np.linalg.norm(ref.ravel())
+        spm, _ = _oracle.render(scene, integ, args.spp, np.array(done[: min(len(done), 8)], dtype=np.int32),
+                                threads=threads, variant="spm")
+        parity = {"vs": "oracle(glibc libm)", "tiles": len(done), "rel_l2": float(diff / max(norm, 1e-30)),
+                  "bitexact_pixel_frac": float(np.mean(np.all(g == ref, axis=-1))),
+                  "bitexact_vs_spm_oracle": bool(np.array_equal(g[: spm.shape[0]], spm))}
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

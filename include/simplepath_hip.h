@@ -1,0 +1,225 @@
+/*
+ * simplepath_hip.h -- C-ABI boundary of the MI355X-native SimplePath renderer.
+ *
+ * This is the drop-in boundary for the reference's per-pixel integration hot path
+ * (kjeffery/SimplePath, main.cpp:77-107 `render_thread` driving
+ * Integrators/Integrator.h:37 `Integrator::integrate` over
+ * base/TileScheduler.h:29 `TileScheduler::get_next_tile`).  Every entry point takes
+ * plain pointers and sizes; no C++ or torch types cross it.
+ *
+ * Entry points and the reference interface each one replaces:
+ *
+ *   sp_scene_load / sp_scene_load_string  base/FileParser.cpp:929 `sp::parse_file`
+ *                                         + base/Scene.h:59 `Scene::Scene` (accelerators)
+ *   sp_scene_get_info                     base/Scene.h:90-96 (image_width, image_height,
+ *                                         russian_roulette_depth, max_depth, integrator_type)
+ *   sp_scene_get_desc                     the primitive / light / material / camera state
+ *                                         held by base/Scene.h:99-105 (flattened, host memory)
+ *   sp_scene_upload                       (no reference counterpart: HBM residency)
+ *   sp_render_tiles                       main.cpp:77-107 `render_thread`: for each scheduled
+ *                                         tile, for each pixel, num_pixel_samples x
+ *                                         `integrator.integrate(camera.generate_ray(...))`,
+ *                                         averaged -- executed by HIP kernels on the device
+ *   sp_tiles_to_image                     main.cpp:100-102 `image(p.x, p.y) += ... /= spp`
+ *                                         scatter of tile-packed radiance into the Image
+ *   sp_tile_count                         base/TileScheduler.h:38-48 `get_num_tiles`
+ *   sp_tile_origin                        base/TileScheduler.h:72-86 ColumnMajor tile order
+ *   sp_string_to_integrator               Integrators/Integrator.cpp:25 `string_to_integrator_type`
+ *
+ * Error behaviour: every function returns SP_OK (0) or a negative SP_ERR_* code and
+ * records a message retrievable with sp_last_error() (thread-local), mirroring the
+ * reference's exceptions (ParsingException, std::runtime_error("Unknown integrator type")).
+ */
+#ifndef SIMPLEPATH_HIP_H
+#define SIMPLEPATH_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SP_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------- */
+enum {
+    SP_OK               = 0,
+    SP_ERR_PARSE        = -1, /* sp::ParsingException                                 */
+    SP_ERR_IO           = -2, /* unable to open file                                  */
+    SP_ERR_ARG          = -3, /* invalid argument                                     */
+    SP_ERR_HIP          = -4, /* HIP runtime failure / no device                      */
+    SP_ERR_UNSUPPORTED  = -5, /* feature present in the reference but not on this path */
+    SP_ERR_STATE        = -6  /* call order violated (e.g. render before upload)      */
+};
+
+/* ---- integrators: Integrators/Integrator.h:18 IntegratorType ---------------------- */
+enum {
+    SP_INTEGRATOR_NOT_SPECIFIED          = 0,
+    SP_INTEGRATOR_MANDELBROT             = 1,
+    SP_INTEGRATOR_BRUTE_FORCE            = 2,
+    SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE  = 3,
+    SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR = 4,
+    SP_INTEGRATOR_ITERATIVE_RRNEE        = 5,
+    SP_INTEGRATOR_DIRECT_LIGHTING        = 6,
+    SP_INTEGRATOR_WHITTED                = 7
+};
+
+/* ---- flattened scene (host memory, owned by the sp_scene) ------------------------- */
+
+/* AffineSpace (math/AffineSpace.h:12): three columns + translation. */
+typedef struct sp_affine {
+    float vx[3], vy[3], vz[3], p[3];
+} sp_affine;
+
+/* LinearSpace3x3 (math/LinearSpace3x3.h:13): three columns. */
+typedef struct sp_linear {
+    float vx[3], vy[3], vz[3];
+} sp_linear;
+
+/* Material kinds produced by base/FileParser.cpp (materials/Material.h:808-829). */
+enum {
+    SP_MAT_LAMBERTIAN = 0, /* OneSampleMaterial{ LambertianBRDF }                             */
+    SP_MAT_GLOSSY     = 1, /* OneSampleMaterial{ MicrofacetReflection(Beckmann), LambertianBRDF } */
+    SP_MAT_CLEARCOAT  = 2  /* ClearcoatMaterial{ base }                                       */
+};
+
+typedef struct sp_material_desc {
+    int32_t kind;
+    int32_t base;               /* clearcoat: index of base material, else -1                 */
+    float   lambert_albedo[3];  /* LambertianBRDF::m_albedo == albedo / pi (Material.h:317)   */
+    float   microfacet_r[3];    /* MicrofacetReflection::m_r (white)                          */
+    float   alpha_x, alpha_y;   /* BeckmannDistribution alphas (roughness_to_alpha, Material.h:231) */
+    float   microfacet_ior;     /* MicrofacetReflection::m_ior                                */
+    int32_t sample_visible_area;/* MicrofacetDistribution::m_sample_visible_area              */
+    float   coat_ior;           /* ClearcoatMaterial::m_ior                                    */
+    float   coat_color[3];      /* ClearcoatMaterial::m_specular_color                         */
+} sp_material_desc;
+
+/* Primitive kinds in Scene::m_accelerator_geometry order. */
+enum { SP_PRIM_TRIANGLE = 0, SP_PRIM_SPHERE = 1, SP_PRIM_PLANE = 2 };
+
+/* Sphere / Plane (shapes/Shape.h:42 TransformableShape). normal_to_world is
+ * object_to_world.linear.inverse().transposed() -- what LinearSpace3x3::operator()(Normal3)
+ * (math/LinearSpace3x3.h:163) recomputes on every call; here computed once with the same
+ * arithmetic. */
+typedef struct sp_xform_shape {
+    sp_affine object_to_world;
+    sp_affine world_to_object;
+    sp_linear normal_to_world;
+    int32_t   material;
+    int32_t   kind; /* SP_PRIM_SPHERE or SP_PRIM_PLANE */
+} sp_xform_shape;
+
+/* Light kinds (Lights/Light.h). */
+enum { SP_LIGHT_SPHERE = 0, SP_LIGHT_ENVIRONMENT = 1, SP_LIGHT_IMAGE_ENVIRONMENT = 2 };
+
+typedef struct sp_light_desc {
+    int32_t   kind;
+    int32_t   pad;
+    float     radiance[3];
+    sp_affine object_to_world; /* sphere light */
+    sp_affine world_to_object;
+    sp_linear normal_to_world;
+} sp_light_desc;
+
+/* PerspectiveCamera (Cameras/Camera.h:85): the transform built by create_transform. */
+typedef struct sp_camera_desc {
+    sp_affine transform;
+    int32_t   film_width, film_height;
+} sp_camera_desc;
+
+typedef struct sp_scene_info {
+    int32_t image_width, image_height;
+    int32_t russian_roulette_depth, max_depth;
+    int32_t integrator_type; /* SP_INTEGRATOR_* as parsed (0 = not specified)          */
+    int32_t num_triangles, num_vertices, num_shapes, num_lights, num_materials;
+    char    output_file_name[256];
+} sp_scene_info;
+
+typedef struct sp_scene_desc {
+    sp_scene_info          info;
+    sp_camera_desc         camera;
+    /* mesh data: world-space (Mesh ctor pre-transforms, shapes/Triangle.h:25) */
+    const float*           vertices;   /* num_vertices * 3                                   */
+    const float*           normals;    /* num_vertices * 3 (transformed, not re-normalized)  */
+    const uint32_t*        indices;    /* num_triangles * 3                                  */
+    const int32_t*         tri_material;/* num_triangles                                     */
+    const sp_xform_shape*  shapes;     /* num_shapes (spheres, planes)                       */
+    /* Scene::m_geometry order before partitioning: (kind, index) pairs. kind = SP_PRIM_*;
+     * index into triangles or shapes. */
+    const int32_t*         prim_kind;
+    const int32_t*         prim_index;
+    int64_t                num_prims;
+    const sp_light_desc*   lights;     /* Scene::m_lights order                              */
+    const sp_material_desc* materials;
+} sp_scene_desc;
+
+/* ---- render ------------------------------------------------------------------------ */
+
+typedef struct sp_render_params {
+    int32_t        integrator;        /* SP_INTEGRATOR_*; 0 => scene's (DirectLighting if unset: main.cpp:387-392) */
+    uint32_t       samples_per_pixel; /* main.cpp `--samples`                                    */
+    const int32_t* tile_ids;          /* host array of tile indices (ColumnMajor order); NULL => all tiles */
+    int64_t        num_tiles;         /* length of tile_ids (ignored when tile_ids == NULL)      */
+    void*          stream;            /* hipStream_t, NULL = default stream                      */
+    int32_t        bvh_mode;          /* 0 = SAH (fast), 1 = reference median-split order        */
+    int32_t        flags;             /* reserved                                                 */
+} sp_render_params;
+
+typedef struct sp_render_stats {
+    uint64_t rays;            /* every ray cast: camera/extension + shadow + MIS rays            */
+    uint64_t shadow_rays;     /* intersect_p queries                                              */
+    uint64_t samples;         /* pixel samples (paths)                                            */
+    uint64_t rng_draws;       /* IncoherentSampler draws                                          */
+    float    kernel_ms;       /* HIP-event time of the render kernel(s)                           */
+    float    twist_ms;        /* reserved                                                         */
+} sp_render_stats;
+
+/* ---- API ------------------------------------------------------------------------------ */
+typedef struct sp_scene sp_scene;
+
+const char* sp_version(void);
+const char* sp_last_error(void);
+
+int  sp_string_to_integrator(const char* name, int32_t* out);
+
+int  sp_scene_load(const char* path, sp_scene** out);
+int  sp_scene_load_string(const char* text, const char* base_dir, sp_scene** out);
+void sp_scene_free(sp_scene* scene);
+int  sp_scene_get_info(const sp_scene* scene, sp_scene_info* out);
+int  sp_scene_get_desc(const sp_scene* scene, sp_scene_desc* out);
+/* Override image size after load (camera rebuilt as FileParser would with these values). */
+int  sp_scene_set_resolution(sp_scene* scene, int32_t width, int32_t height);
+
+int  sp_tile_count(int32_t width, int32_t height, int64_t* out);
+int  sp_tile_origin(int32_t width, int32_t height, int64_t tile, int32_t* x0, int32_t* y0);
+
+/* Device side. */
+int  sp_device_count(int32_t* out);
+int  sp_scene_upload(sp_scene* scene, int32_t device, int32_t bvh_mode);
+/* Render tiles into a DEVICE buffer laid out tile-packed: out[(slot*64 + morton)*3 + c],
+ * slot = position of the tile in params->tile_ids (or the tile index itself when NULL).
+ * Pixels of clipped border tiles that fall outside the image are written as 0. */
+int  sp_render_tiles(sp_scene* scene, const sp_render_params* params, float* d_out,
+                     sp_render_stats* stats);
+/* Same as sp_render_tiles but allocates the device buffer itself and copies the tile-packed
+ * radiance back into h_out (num_tiles * 64 * 3 floats). */
+int  sp_render_tiles_host(sp_scene* scene, const sp_render_params* params, float* h_out,
+                          sp_render_stats* stats);
+/* BVH statistics of the uploaded scene (depth, node count, primitive slots). */
+int  sp_scene_bvh_info(const sp_scene* scene, int32_t* depth, int64_t* nodes, int64_t* slots);
+/* Scatter tile-packed radiance (host memory) into a row-major width x height x 3 image. */
+int  sp_tiles_to_image(int32_t width, int32_t height, const int32_t* tile_ids, int64_t num_tiles,
+                       const float* tiles, float* image);
+/* Write an image as PFM exactly as Image/Image.cpp:40 write_pfm does. */
+int  sp_write_pfm(const char* path, int32_t width, int32_t height, const float* image);
+
+/* Numerics self-checks used by the tests (no GPU needed). */
+int  sp_rsqrt_table_info(int32_t* mantissa_bits, int32_t* verified);
+float sp_host_rsqrt_emulated(float x); /* table emulation of RSQRTSS, host-evaluated */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIMPLEPATH_HIP_H */

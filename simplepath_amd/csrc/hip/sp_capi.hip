@@ -1,0 +1,617 @@
+// sp_capi.hip -- extern "C" boundary (include/simplepath_hip.h) and HBM residency of scenes.
+#include "sp_device.hpp"
+#include "../host/sp_host.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace spd {
+hipError_t launch_render(const Scene& sc, const RenderArgs& args, int blocks, size_t lds_bytes, hipStream_t stream);
+int        render_blocks_per_cu(size_t lds_bytes);
+} // namespace spd
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define SP_HIP(call)                                                                                      \
+    do {                                                                                                  \
+        hipError_t e__ = (call);                                                                          \
+        if (e__ != hipSuccess) return fail(SP_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e__)); \
+    } while (0)
+
+constexpr int MAX_RECURSION = 32; // sp_render.hip integrate_bruteforce / integrate_whitted
+
+uint32_t code_of(int kind, int index) { return ((uint32_t)kind << spd::CODE_SHIFT) | (uint32_t)index; }
+
+// BBox3 of a primitive (shapes/Triangle.h:228, shapes/Shape.h:290 for transformed shapes)
+sph::PrimBounds tri_bounds(const sph::Scene& s, int t)
+{
+    sph::PrimBounds b;
+    for (int i = 0; i < 3; ++i) { b.lo[i] = INFINITY; b.hi[i] = -INFINITY; }
+    for (int k = 0; k < 3; ++k) {
+        const spm::f3 p   = s.vertices[s.indices[3 * t + k]];
+        const float   v[3] = { p.x, p.y, p.z };
+        for (int i = 0; i < 3; ++i) {
+            b.lo[i] = spm::sse_min(v[i], b.lo[i]); // BBox::extend: min(p, m_min)
+            b.hi[i] = spm::sse_max(v[i], b.hi[i]);
+        }
+    }
+    return b;
+}
+
+spm::aff from_desc(const sp_affine& d)
+{
+    spm::aff a;
+    a.vx = spm::mk(d.vx[0], d.vx[1], d.vx[2]);
+    a.vy = spm::mk(d.vy[0], d.vy[1], d.vy[2]);
+    a.vz = spm::mk(d.vz[0], d.vz[1], d.vz[2]);
+    a.p  = spm::mk(d.p[0], d.p[1], d.p[2]);
+    return a;
+}
+spm::lin from_desc(const sp_linear& d)
+{
+    spm::lin a;
+    a.vx = spm::mk(d.vx[0], d.vx[1], d.vx[2]);
+    a.vy = spm::mk(d.vy[0], d.vy[1], d.vy[2]);
+    a.vz = spm::mk(d.vz[0], d.vz[1], d.vz[2]);
+    return a;
+}
+
+sph::PrimBounds sphere_bounds(const spm::aff& o2w)
+{
+    sph::PrimBounds b;
+    for (int i = 0; i < 3; ++i) { b.lo[i] = INFINITY; b.hi[i] = -INFINITY; }
+    // AffineSpace::operator()(BBox3) (math/AffineSpace.h:104): corners p0..p7
+    const float lo = -1.0f, hi = 1.0f;
+    const float cs[8][3] = { { lo, lo, lo }, { lo, lo, hi }, { lo, hi, lo }, { lo, hi, hi },
+                             { hi, lo, lo }, { hi, lo, hi }, { hi, hi, lo }, { hi, hi, hi } };
+    for (auto& c : cs) {
+        const spm::f3 p    = spm::xfm_point(o2w, spm::mk(c[0], c[1], c[2]));
+        const float   v[3] = { p.x, p.y, p.z };
+        for (int i = 0; i < 3; ++i) {
+            b.lo[i] = spm::sse_min(v[i], b.lo[i]);
+            b.hi[i] = spm::sse_max(v[i], b.hi[i]);
+        }
+    }
+    return b;
+}
+
+struct DevBuf {
+    void*  p     = nullptr;
+    size_t bytes = 0;
+};
+} // namespace
+
+struct sp_scene {
+    std::unique_ptr<sph::Scene> host;
+    sp_scene_desc               desc{};
+    // device residency
+    int                  device   = -1;
+    int                  bvh_mode = -1;
+    std::vector<DevBuf>  bufs;
+    spd::Scene           dev{};
+    int                  geom_depth = 0, light_depth = 0;
+    size_t               geom_nodes = 0, geom_slots = 0;
+    // render scratch
+    uint64_t*            mt_state     = nullptr;
+    size_t               mt_waves     = 0;
+    int32_t*             tile_counter = nullptr;
+    unsigned long long*  counters     = nullptr;
+    int32_t*             d_tiles      = nullptr;
+    size_t               d_tiles_cap  = 0;
+    hipEvent_t           ev0 = nullptr, ev1 = nullptr;
+
+    void release()
+    {
+        if (device >= 0) (void)hipSetDevice(device);
+        for (auto& b : bufs) (void)hipFree(b.p);
+        bufs.clear();
+        if (mt_state) (void)hipFree(mt_state);
+        if (tile_counter) (void)hipFree(tile_counter);
+        if (counters) (void)hipFree(counters);
+        if (d_tiles) (void)hipFree(d_tiles);
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
+        ev0 = ev1 = nullptr;
+        mt_waves = 0; d_tiles_cap = 0;
+        device = -1; bvh_mode = -1;
+    }
+    ~sp_scene() { release(); }
+
+    template <typename T>
+    int upload(const std::vector<T>& v, const T** out)
+    {
+        *out = nullptr;
+        if (v.empty()) return SP_OK;
+        DevBuf b;
+        b.bytes = v.size() * sizeof(T);
+        SP_HIP(hipMalloc(&b.p, b.bytes));
+        SP_HIP(hipMemcpy(b.p, v.data(), b.bytes, hipMemcpyHostToDevice));
+        bufs.push_back(b);
+        *out = static_cast<const T*>(b.p);
+        return SP_OK;
+    }
+};
+
+namespace {
+void fill_desc(sp_scene* s)
+{
+    const sph::Scene& h = *s->host;
+    sp_scene_desc&    d = s->desc;
+    d                   = sp_scene_desc{};
+    d.info.image_width  = h.image_width;
+    d.info.image_height = h.image_height;
+    d.info.russian_roulette_depth = h.rr_depth;
+    d.info.max_depth              = h.max_depth;
+    d.info.integrator_type        = h.integrator;
+    d.info.num_triangles          = static_cast<int32_t>(h.tri_material.size());
+    d.info.num_vertices           = static_cast<int32_t>(h.vertices.size());
+    d.info.num_shapes             = static_cast<int32_t>(h.shapes.size());
+    d.info.num_lights             = static_cast<int32_t>(h.lights.size());
+    d.info.num_materials          = static_cast<int32_t>(h.materials.size());
+    std::strncpy(d.info.output_file_name, h.output_file_name.c_str(), sizeof(d.info.output_file_name) - 1);
+    auto put = [](float* o, spm::f3 v) { o[0] = v.x; o[1] = v.y; o[2] = v.z; };
+    put(d.camera.transform.vx, h.camera.vx);
+    put(d.camera.transform.vy, h.camera.vy);
+    put(d.camera.transform.vz, h.camera.vz);
+    put(d.camera.transform.p, h.camera.p);
+    d.camera.film_width  = h.image_width;
+    d.camera.film_height = h.image_height;
+    static_assert(sizeof(spm::f3) == 12, "f3 packing");
+    d.vertices     = h.vertices.empty() ? nullptr : &h.vertices[0].x;
+    d.normals      = h.normals.empty() ? nullptr : &h.normals[0].x;
+    d.indices      = h.indices.empty() ? nullptr : h.indices.data();
+    d.tri_material = h.tri_material.empty() ? nullptr : h.tri_material.data();
+    d.shapes       = h.shapes.empty() ? nullptr : h.shapes.data();
+    d.prim_kind    = h.prim_kind.empty() ? nullptr : h.prim_kind.data();
+    d.prim_index   = h.prim_index.empty() ? nullptr : h.prim_index.data();
+    d.num_prims    = static_cast<int64_t>(h.prim_kind.size());
+    d.lights       = h.lights.empty() ? nullptr : h.lights.data();
+    static std::vector<sp_material_desc> dummy;
+    (void)dummy;
+}
+
+std::vector<sp_material_desc> material_descs(const sph::Scene& h)
+{
+    std::vector<sp_material_desc> m;
+    for (auto& x : h.materials) m.push_back(x.d);
+    return m;
+}
+
+int wrap_load(std::unique_ptr<sph::Scene> (*fn)(const std::string&, const std::string&), const std::string& a,
+              const std::string& b, sp_scene** out)
+{
+    try {
+        auto* s = new sp_scene;
+        s->host = fn(a, b);
+        fill_desc(s);
+        *out = s;
+        return SP_OK;
+    } catch (const sph::SpError& e) {
+        return fail(e.code, e.what());
+    } catch (const std::exception& e) {
+        return fail(SP_ERR_PARSE, std::string("Unexpected file parsing error: ") + e.what());
+    }
+}
+} // namespace
+
+extern "C" {
+
+const char* sp_version(void) { return "simplepath-amd 0.1 (gfx950)"; }
+const char* sp_last_error(void) { return g_last_error.c_str(); }
+
+int sp_string_to_integrator(const char* name, int32_t* out)
+{
+    if (!name || !out) return fail(SP_ERR_ARG, "null argument");
+    std::string s(name);
+    while (!s.empty() && std::isspace(static_cast<unsigned char>(s.back()))) s.pop_back();
+    size_t b = 0;
+    while (b < s.size() && std::isspace(static_cast<unsigned char>(s[b]))) ++b;
+    s = s.substr(b);
+    // Integrators/Integrator.cpp:25 string_to_integrator_type
+    if (s == "mandelbrot") *out = SP_INTEGRATOR_MANDELBROT;
+    else if (s == "brute_force") *out = SP_INTEGRATOR_BRUTE_FORCE;
+    else if (s == "brute_force_iterative") *out = SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE;
+    else if (s == "brute_force_iterative_rr") *out = SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR;
+    else if (s == "iterative_rrnee") *out = SP_INTEGRATOR_ITERATIVE_RRNEE;
+    else if (s == "direct_lighting") *out = SP_INTEGRATOR_DIRECT_LIGHTING;
+    else if (s == "whitted") *out = SP_INTEGRATOR_WHITTED;
+    else return fail(SP_ERR_ARG, "Unknown integrator type");
+    return SP_OK;
+}
+
+int sp_scene_load(const char* path, sp_scene** out)
+{
+    if (!path || !out) return fail(SP_ERR_ARG, "null argument");
+    return wrap_load([](const std::string& p, const std::string&) { return sph::parse_scene_file(p); }, path, "", out);
+}
+
+int sp_scene_load_string(const char* text, const char* base_dir, sp_scene** out)
+{
+    if (!text || !out) return fail(SP_ERR_ARG, "null argument");
+    return wrap_load(&sph::parse_scene, text, base_dir ? base_dir : ".", out);
+}
+
+void sp_scene_free(sp_scene* scene) { delete scene; }
+
+int sp_scene_get_info(const sp_scene* scene, sp_scene_info* out)
+{
+    if (!scene || !out) return fail(SP_ERR_ARG, "null argument");
+    *out = scene->desc.info;
+    return SP_OK;
+}
+
+int sp_scene_get_desc(const sp_scene* scene, sp_scene_desc* out)
+{
+    if (!scene || !out) return fail(SP_ERR_ARG, "null argument");
+    static thread_local std::vector<sp_material_desc> mats;
+    mats       = material_descs(*scene->host);
+    *out       = scene->desc;
+    out->materials = mats.empty() ? nullptr : mats.data();
+    return SP_OK;
+}
+
+int sp_scene_set_resolution(sp_scene* scene, int32_t width, int32_t height)
+{
+    if (!scene || width <= 0 || height <= 0 || width > 65535 || height > 65535) return fail(SP_ERR_ARG, "bad resolution");
+    scene->host->image_width  = width;
+    scene->host->image_height = height;
+    scene->host->rebuild_camera();
+    fill_desc(scene);
+    if (scene->device >= 0) {
+        scene->dev.width  = width;
+        scene->dev.height = height;
+        scene->dev.camera = scene->host->camera;
+    }
+    return SP_OK;
+}
+
+int sp_tile_count(int32_t width, int32_t height, int64_t* out)
+{
+    if (!out || width < 0 || height < 0) return fail(SP_ERR_ARG, "bad argument");
+    *out = (int64_t)((width + 7) / 8) * ((height + 7) / 8);
+    return SP_OK;
+}
+
+int sp_tile_origin(int32_t width, int32_t height, int64_t tile, int32_t* x0, int32_t* y0)
+{
+    int64_t n;
+    sp_tile_count(width, height, &n);
+    if (tile < 0 || tile >= n || !x0 || !y0) return fail(SP_ERR_ARG, "tile out of range");
+    const int32_t w = (width + 7) / 8;
+    *x0             = (int32_t)(tile % w) * 8;
+    *y0             = (int32_t)(tile / w) * 8;
+    return SP_OK;
+}
+
+int sp_device_count(int32_t* out)
+{
+    if (!out) return fail(SP_ERR_ARG, "null argument");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return SP_OK;
+}
+
+int sp_rsqrt_table_info(int32_t* mantissa_bits, int32_t* verified)
+{
+    const auto& c = sph::rsqrt_capture();
+    if (mantissa_bits) *mantissa_bits = c.bits;
+    if (verified) *verified = c.verified ? 1 : 0;
+    return SP_OK;
+}
+
+float sp_host_rsqrt_emulated(float x)
+{
+    const auto&     c = sph::rsqrt_capture();
+    spm::RsqrtTable t{ c.entries.data(), c.bits, c.zero_result, c.denorm_result };
+    return spm::rsqrtss_emulated(x, t);
+}
+
+int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
+{
+    if (!s) return fail(SP_ERR_ARG, "null scene");
+    if (bvh_mode != 0 && bvh_mode != 1) return fail(SP_ERR_ARG, "bvh_mode must be 0 (SAH) or 1 (reference)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SP_ERR_HIP, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(SP_ERR_ARG, "device out of range");
+    if (s->device == device && s->bvh_mode == bvh_mode) return SP_OK;
+    s->release();
+    SP_HIP(hipSetDevice(device));
+    s->device   = device;
+    s->bvh_mode = bvh_mode;
+    const sph::Scene& h = *s->host;
+    spd::Scene&       d = s->dev;
+    d                   = spd::Scene{};
+
+    const auto& rc = sph::rsqrt_capture();
+    if (rc.entries.empty()) return fail(SP_ERR_UNSUPPORTED, "RSQRTSS table capture failed");
+    if (!rc.verified) return fail(SP_ERR_UNSUPPORTED, "RSQRTSS table could not be verified on this host CPU");
+
+    // ---- materials (nested clearcoat is not produced by the scenes on this path)
+    std::vector<spd::Material> mats;
+    for (auto& m : h.materials) {
+        spd::Material x{};
+        x.kind           = m.d.kind;
+        x.base           = m.d.base;
+        x.lambert_albedo = spm::mkc(m.d.lambert_albedo[0], m.d.lambert_albedo[1], m.d.lambert_albedo[2]);
+        x.microfacet_r   = spm::mkc(m.d.microfacet_r[0], m.d.microfacet_r[1], m.d.microfacet_r[2]);
+        x.alpha_x        = m.d.alpha_x;
+        x.alpha_y        = m.d.alpha_y;
+        x.microfacet_ior = m.d.microfacet_ior;
+        x.sample_visible_area = m.d.sample_visible_area;
+        x.coat_ior       = m.d.coat_ior;
+        x.coat_color     = spm::mkc(m.d.coat_color[0], m.d.coat_color[1], m.d.coat_color[2]);
+        if (x.kind == SP_MAT_CLEARCOAT && h.materials[x.base].d.kind == SP_MAT_CLEARCOAT)
+            return fail(SP_ERR_UNSUPPORTED, "clearcoat over clearcoat");
+        mats.push_back(x);
+    }
+
+    // ---- geometry: Scene ctor partition (base/Scene.h:29) then BVH over the bounded part
+    std::vector<int32_t> prims(h.prim_kind.size());
+    for (size_t i = 0; i < prims.size(); ++i) prims[i] = (int32_t)i;
+    const size_t part = sph::stl_partition(prims, 0, prims.size(),
+                                           [&](int32_t p) { return h.prim_kind[p] != SP_PRIM_PLANE; });
+    std::vector<sph::PrimBounds> bounds;
+    std::vector<spd::Shape>      shapes;
+    for (auto& sh : h.shapes) {
+        spd::Shape x{};
+        x.o2w      = from_desc(sh.object_to_world);
+        x.w2o      = from_desc(sh.world_to_object);
+        x.nrm      = from_desc(sh.normal_to_world);
+        x.material = sh.material;
+        x.kind     = sh.kind;
+        shapes.push_back(x);
+    }
+    for (size_t i = 0; i < part; ++i) {
+        const int32_t p = prims[i];
+        if (h.prim_kind[p] == SP_PRIM_TRIANGLE) bounds.push_back(tri_bounds(h, h.prim_index[p]));
+        else bounds.push_back(sphere_bounds(shapes[h.prim_index[p]].o2w));
+    }
+    std::vector<int32_t> unbounded;
+    for (size_t i = part; i < prims.size(); ++i) unbounded.push_back(h.prim_index[prims[i]]);
+    const sph::Bvh bvh = (bvh_mode == 1) ? sph::build_bvh_reference(bounds) : sph::build_bvh_sah(bounds, 4);
+    std::vector<float4>   slot_tri(bvh.prim_order.size() * 3);
+    std::vector<uint32_t> slot_code(bvh.prim_order.size());
+    for (size_t sl = 0; sl < bvh.prim_order.size(); ++sl) {
+        const int32_t p    = prims[bvh.prim_order[sl]];
+        const int     kind = h.prim_kind[p];
+        const int     idx  = h.prim_index[p];
+        slot_code[sl]      = code_of(kind, idx);
+        if (kind == SP_PRIM_TRIANGLE) {
+            for (int k = 0; k < 3; ++k) {
+                const spm::f3 v  = h.vertices[h.indices[3 * idx + k]];
+                slot_tri[3 * sl + k] = make_float4(v.x, v.y, v.z, 0.0f);
+            }
+        }
+    }
+    std::vector<spd::Node> nodes(bvh.nodes.size());
+    static_assert(sizeof(spd::Node) == sizeof(sph::BvhNode), "node layout");
+    std::memcpy(nodes.data(), bvh.nodes.data(), nodes.size() * sizeof(spd::Node));
+
+    // ---- lights: Scene::m_lights order + accelerator (partition by boundedness)
+    std::vector<spd::Light> lights;
+    for (auto& l : h.lights) {
+        spd::Light x{};
+        x.kind     = l.kind;
+        x.radiance = spm::mkc(l.radiance[0], l.radiance[1], l.radiance[2]);
+        x.o2w      = from_desc(l.object_to_world);
+        x.w2o      = from_desc(l.world_to_object);
+        x.nrm      = from_desc(l.normal_to_world);
+        lights.push_back(x);
+    }
+    std::vector<int32_t> lids(lights.size());
+    for (size_t i = 0; i < lids.size(); ++i) lids[i] = (int32_t)i;
+    const size_t lpart = sph::stl_partition(lids, 0, lids.size(), [&](int32_t i) { return lights[i].kind == SP_LIGHT_SPHERE; });
+    std::vector<sph::PrimBounds> lbounds;
+    for (size_t i = 0; i < lpart; ++i) lbounds.push_back(sphere_bounds(lights[lids[i]].o2w));
+    std::vector<int32_t> unbounded_lights(lids.begin() + (long)lpart, lids.end());
+    const sph::Bvh lbvh = sph::build_bvh_reference(lbounds);
+    std::vector<uint32_t> light_slot(lbvh.prim_order.size());
+    for (size_t sl = 0; sl < light_slot.size(); ++sl) light_slot[sl] = (uint32_t)lids[lbvh.prim_order[sl]];
+    std::vector<spd::Node> lnodes(lbvh.nodes.size());
+    std::memcpy(lnodes.data(), lbvh.nodes.data(), lnodes.size() * sizeof(spd::Node));
+
+    // ---- upload
+    int rc2 = SP_OK;
+    auto up = [&](auto& vec, auto** ptr) { if (rc2 == SP_OK) rc2 = s->upload(vec, ptr); };
+    d.camera    = h.camera;
+    d.width     = h.image_width;
+    d.height    = h.image_height;
+    d.max_depth = h.max_depth;
+    d.rr_depth  = h.rr_depth;
+    float a1[1], a2[2];
+    sph::rsequence_alphas(a1, a2);
+    d.alpha2_0 = a2[0];
+    d.alpha2_1 = a2[1];
+    d.n_unbounded = (int)unbounded.size();
+    up(unbounded, &d.unbounded);
+    d.n_nodes = (int)nodes.size();
+    up(nodes, &d.nodes);
+    up(slot_tri, &d.slot_tri);
+    up(slot_code, &d.slot_code);
+    std::vector<float> nrm(h.normals.size() * 3);
+    for (size_t i = 0; i < h.normals.size(); ++i) { nrm[3 * i] = h.normals[i].x; nrm[3 * i + 1] = h.normals[i].y; nrm[3 * i + 2] = h.normals[i].z; }
+    up(nrm, &d.normals);
+    up(h.indices, &d.indices);
+    up(h.tri_material, &d.tri_material);
+    up(shapes, &d.shapes);
+    d.n_lights = (int)lights.size();
+    up(lights, &d.lights);
+    d.n_unbounded_lights = (int)unbounded_lights.size();
+    up(unbounded_lights, &d.unbounded_lights);
+    d.n_light_nodes = (int)lnodes.size();
+    up(lnodes, &d.light_nodes);
+    up(light_slot, &d.light_slot);
+    up(mats, &d.materials);
+    up(rc.entries, &d.rsqrt_entries);
+    if (rc2 != SP_OK) return rc2;
+    d.rsqrt_bits   = rc.bits;
+    d.rsqrt_zero   = rc.zero_result;
+    d.rsqrt_denorm = rc.denorm_result;
+    s->geom_depth  = bvh.max_depth;
+    s->light_depth = lbvh.max_depth;
+    s->geom_nodes  = nodes.size();
+    s->geom_slots  = slot_code.size();
+    d.stack_depth  = std::max(bvh.max_depth, lbvh.max_depth) + 1;
+    SP_HIP(hipMalloc(&s->tile_counter, sizeof(int32_t)));
+    SP_HIP(hipMalloc(&s->counters, 4 * sizeof(unsigned long long)));
+    SP_HIP(hipEventCreate(&s->ev0));
+    SP_HIP(hipEventCreate(&s->ev1));
+    return SP_OK;
+}
+
+int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats)
+{
+    if (!s || !p || !d_out) return fail(SP_ERR_ARG, "null argument");
+    if (s->device < 0) return fail(SP_ERR_STATE, "sp_scene_upload must be called before sp_render_tiles");
+    if (p->samples_per_pixel == 0) return fail(SP_ERR_ARG, "samples_per_pixel must be > 0");
+    SP_HIP(hipSetDevice(s->device));
+    int32_t integ = p->integrator;
+    if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = s->host->integrator;
+    if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = SP_INTEGRATOR_DIRECT_LIGHTING; // main.cpp:390
+    if (integ < SP_INTEGRATOR_MANDELBROT || integ > SP_INTEGRATOR_WHITTED) return fail(SP_ERR_ARG, "Unknown integrator type");
+    if (integ == SP_INTEGRATOR_MANDELBROT) return fail(SP_ERR_UNSUPPORTED, "mandelbrot integrator is not on the device path yet");
+    if ((integ == SP_INTEGRATOR_BRUTE_FORCE || integ == SP_INTEGRATOR_WHITTED) && s->host->max_depth > MAX_RECURSION)
+        return fail(SP_ERR_UNSUPPORTED, "recursive integrators support max_depth <= 32");
+    int64_t total;
+    sp_tile_count(s->dev.width, s->dev.height, &total);
+    const int64_t n_tiles = p->tile_ids ? p->num_tiles : total;
+    if (n_tiles < 0) return fail(SP_ERR_ARG, "num_tiles < 0");
+    if (p->tile_ids)
+        for (int64_t i = 0; i < n_tiles; ++i)
+            if (p->tile_ids[i] < 0 || p->tile_ids[i] >= total) return fail(SP_ERR_ARG, "tile id out of range");
+    hipStream_t stream = static_cast<hipStream_t>(p->stream);
+    if (stats) *stats = sp_render_stats{};
+    if (n_tiles == 0) return SP_OK;
+    if (p->tile_ids) {
+        if ((size_t)n_tiles > s->d_tiles_cap) {
+            if (s->d_tiles) (void)hipFree(s->d_tiles);
+            s->d_tiles = nullptr;
+            SP_HIP(hipMalloc(&s->d_tiles, (size_t)n_tiles * sizeof(int32_t)));
+            s->d_tiles_cap = (size_t)n_tiles;
+        }
+        SP_HIP(hipMemcpyAsync(s->d_tiles, p->tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+    }
+    const int    rs_words  = 2 << s->dev.rsqrt_bits;
+    const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_depth * 64 * 4;
+    if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+    hipDeviceProp_t prop;
+    SP_HIP(hipGetDeviceProperties(&prop, s->device));
+    const int     per_cu  = spd::render_blocks_per_cu(lds_bytes);
+    const int64_t max_blk = (int64_t)prop.multiProcessorCount * per_cu;
+    const int64_t need    = (n_tiles + 3) / 4;
+    const int     blocks  = (int)std::max<int64_t>(1, std::min(max_blk, need));
+    const size_t  waves   = (size_t)blocks * 4;
+    if (waves > s->mt_waves) {
+        if (s->mt_state) (void)hipFree(s->mt_state);
+        s->mt_state = nullptr;
+        SP_HIP(hipMalloc(&s->mt_state, waves * 2 * spm::MT_N * 64 * sizeof(uint64_t)));
+        s->mt_waves = waves;
+    }
+    SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
+    SP_HIP(hipMemsetAsync(s->counters, 0, 4 * sizeof(unsigned long long), stream));
+    spd::RenderArgs a{};
+    a.out          = d_out;
+    a.tile_ids     = p->tile_ids ? s->d_tiles : nullptr;
+    a.num_tiles    = n_tiles;
+    a.tiles_x      = (s->dev.width + 7) / 8;
+    a.spp          = p->samples_per_pixel;
+    a.integrator   = integ;
+    a.tile_counter = s->tile_counter;
+    a.mt_state     = s->mt_state;
+    a.counters     = s->counters;
+    SP_HIP(hipEventRecord(s->ev0, stream));
+    SP_HIP(spd::launch_render(s->dev, a, blocks, lds_bytes, stream));
+    SP_HIP(hipEventRecord(s->ev1, stream));
+    SP_HIP(hipEventSynchronize(s->ev1));
+    if (stats) {
+        unsigned long long c[4];
+        SP_HIP(hipMemcpy(c, s->counters, sizeof(c), hipMemcpyDeviceToHost));
+        float ms = 0.0f;
+        SP_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        stats->rays        = c[0];
+        stats->shadow_rays = c[1];
+        stats->samples     = c[2];
+        stats->rng_draws   = c[3];
+        stats->kernel_ms   = ms;
+    }
+    return SP_OK;
+}
+
+int sp_render_tiles_host(sp_scene* s, const sp_render_params* p, float* h_out, sp_render_stats* stats)
+{
+    if (!s || !p || !h_out) return fail(SP_ERR_ARG, "null argument");
+    if (s->device < 0) return fail(SP_ERR_STATE, "sp_scene_upload must be called before rendering");
+    SP_HIP(hipSetDevice(s->device));
+    int64_t total;
+    sp_tile_count(s->dev.width, s->dev.height, &total);
+    const int64_t n     = p->tile_ids ? p->num_tiles : total;
+    const size_t  bytes = (size_t)std::max<int64_t>(n, 1) * 64 * 3 * sizeof(float);
+    float*        d     = nullptr;
+    SP_HIP(hipMalloc(&d, bytes));
+    int rc = sp_render_tiles(s, p, d, stats);
+    if (rc == SP_OK) {
+        hipError_t e = hipMemcpy(h_out, d, (size_t)n * 64 * 3 * sizeof(float), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(SP_ERR_HIP, hipGetErrorString(e));
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
+int sp_tiles_to_image(int32_t width, int32_t height, const int32_t* tile_ids, int64_t num_tiles, const float* tiles,
+                      float* image)
+{
+    if (!tiles || !image || width <= 0 || height <= 0) return fail(SP_ERR_ARG, "bad argument");
+    int64_t total;
+    sp_tile_count(width, height, &total);
+    const int64_t n  = tile_ids ? num_tiles : total;
+    const int32_t tw = (width + 7) / 8;
+    for (int64_t sl = 0; sl < n; ++sl) {
+        const int64_t t = tile_ids ? tile_ids[sl] : sl;
+        if (t < 0 || t >= total) return fail(SP_ERR_ARG, "tile id out of range");
+        const int32_t x0 = (int32_t)(t % tw) * 8, y0 = (int32_t)(t / tw) * 8;
+        for (uint32_t m = 0; m < 64; ++m) {
+            uint32_t a = m & 0x55u, b = (m >> 1) & 0x55u;
+            a = (a | (a >> 1)) & 0x33u; a = (a | (a >> 2)) & 0x0fu;
+            b = (b | (b >> 1)) & 0x33u; b = (b | (b >> 2)) & 0x0fu;
+            const int32_t x = x0 + (int32_t)a, y = y0 + (int32_t)b;
+            if (x >= width || y >= height) continue;
+            for (int c = 0; c < 3; ++c) image[((size_t)y * width + x) * 3 + c] = tiles[((size_t)sl * 64 + m) * 3 + c];
+        }
+    }
+    return SP_OK;
+}
+
+int sp_write_pfm(const char* path, int32_t width, int32_t height, const float* image)
+{
+    if (!path || !image) return fail(SP_ERR_ARG, "null argument");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(SP_ERR_IO, std::string("Unable to open ") + path);
+    std::fprintf(f, "PF\n%d %d\n%d\n", width, height, -1);
+    for (int32_t j = height - 1; j >= 0; --j)
+        std::fwrite(image + (size_t)j * width * 3, sizeof(float), (size_t)width * 3, f);
+    std::fclose(f);
+    return SP_OK;
+}
+
+int sp_scene_bvh_info(const sp_scene* s, int32_t* depth, int64_t* nodes, int64_t* slots)
+{
+    if (!s || s->device < 0) return fail(SP_ERR_STATE, "scene not uploaded");
+    if (depth) *depth = s->geom_depth;
+    if (nodes) *nodes = (int64_t)s->geom_nodes;
+    if (slots) *slots = (int64_t)s->geom_slots;
+    return SP_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,103 @@
+// sp_device.hpp -- device-resident scene layout and per-lane samplers (gfx950).
+//
+// Layout in HBM (all arrays allocated once per scene upload, read-only during rendering):
+//   nodes/light_nodes : 32-byte binary BVH nodes (sp_host.hpp BvhNode)
+//   slot_tri          : per BVH leaf slot, 3 x float4 {p0|code, p1, p2} -- the triangle's three
+//                       world-space vertices in leaf order, one 48-byte contiguous read per test
+//   slot_code         : per leaf slot, primitive code (kind << 30 | index)
+//   normals/indices   : vertex normals and triangle indices, read once per closest hit
+//   mt_state          : per persistent wave slot, 2 x 312 x 64 uint64 MT19937-64 words,
+//                       [buffer][word][lane] so twists are coalesced 512-byte row accesses
+#pragma once
+#include "../common/sp_libm.h"
+#include "../common/sp_rng.h"
+#include "../../../include/simplepath_hip.h"
+
+namespace spd {
+
+using spm::aff;
+using spm::f3;
+using spm::lin;
+using spm::rgb;
+
+constexpr uint32_t LEAF_BIT   = 0x80000000u;
+constexpr uint32_t CODE_SHIFT = 30;
+constexpr uint32_t CODE_MASK  = (1u << CODE_SHIFT) - 1u;
+
+struct Node {
+    float    lo[3];
+    uint32_t a;
+    float    hi[3];
+    uint32_t b;
+};
+
+struct Shape { // sphere / plane
+    aff      o2w, w2o;
+    lin      nrm; // normal_to_world
+    int32_t  material, kind;
+};
+
+struct Light {
+    int32_t kind, pad;
+    rgb     radiance;
+    aff     o2w, w2o;
+    lin     nrm;
+};
+
+struct Material {
+    int32_t kind, base;
+    rgb     lambert_albedo;
+    rgb     microfacet_r;
+    float   alpha_x, alpha_y, microfacet_ior;
+    int32_t sample_visible_area;
+    float   coat_ior;
+    rgb     coat_color;
+};
+
+struct Scene {
+    aff   camera;
+    int   width, height, max_depth, rr_depth;
+    float alpha2_0, alpha2_1;
+
+    // geometry: Scene::m_accelerator_geometry = ListAccelerator{unbounded..., BVH}
+    int             n_unbounded;
+    const int32_t*  unbounded; // shape indices (planes), reference partition order
+    int             n_nodes;
+    const Node*     nodes;
+    const float4*   slot_tri;  // 3 per slot
+    const uint32_t* slot_code;
+    const float*    normals;   // 3 per vertex
+    const uint32_t* indices;   // 3 per triangle
+    const int32_t*  tri_material;
+    const Shape*    shapes;
+
+    // lights: Scene::m_lights order + m_accelerator_lights
+    int             n_lights;
+    const Light*    lights;
+    int             n_unbounded_lights;
+    const int32_t*  unbounded_lights;
+    int             n_light_nodes;
+    const Node*     light_nodes;
+    const uint32_t* light_slot; // slot -> light index
+
+    const Material* materials;
+
+    const uint32_t* rsqrt_entries; // 2 << rsqrt_bits
+    int32_t         rsqrt_bits;
+    uint32_t        rsqrt_zero, rsqrt_denorm;
+    int             stack_depth;   // LDS traversal stack entries per lane
+};
+
+struct RenderArgs {
+    float*          out;        // tile-packed radiance
+    const int32_t*  tile_ids;   // nullptr => identity
+    int64_t         num_tiles;
+    int32_t         tiles_x;
+    uint32_t        spp;
+    int32_t         integrator;
+    int32_t*        tile_counter;
+    uint64_t*       mt_state;
+    unsigned long long* counters; // [rays, shadow_rays, samples, draws]
+};
+
+} // namespace spd

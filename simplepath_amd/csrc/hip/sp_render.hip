@@ -1,0 +1,1358 @@
+// sp_render.hip -- per-pixel path integration on gfx950 (MI355X), bit-exact with the reference.
+//
+// One 64-lane wave renders one 8x8 tile (base/Tile.h:10 k_tile_dimension = 8), lane = Morton
+// index inside the tile (base/Tile.h TilePixelIterator), exactly the pixel order of
+// main.cpp:91.  Waves are persistent: each grabs tiles from an atomic queue until the list is
+// drained (the device analogue of TileScheduler::get_next_tile), so a single launch covers the
+// frame with no tail of idle CUs.  Each lane runs the reference's sample loop for its pixel
+// (main.cpp:94-102): R2 pixel jitter -> PerspectiveCamera ray -> Integrator -> running sum ->
+// divide by spp.  The pixel's std::mt19937_64 lives in HBM as two 312-word generations; the
+// next generation is twisted ahead of need at wave-synchronous points so lanes rarely twist
+// alone.
+//
+// Numerics: every float operation follows the reference's order; FMAs only where the reference
+// issues them (sp_math.h).  Build flags: -ffp-contract=off, IEEE division/sqrt, denormals kept.
+#include "sp_device.hpp"
+
+namespace spd {
+
+using namespace spm;
+
+// ============================================================================ per-lane state
+struct Rsq {
+    const uint32_t* t;
+    int32_t         bits;
+    uint32_t        zero, denorm;
+};
+
+__device__ __forceinline__ float rsqrt_ref(float a, const Rsq& q)
+{
+    RsqrtTable tb{ q.t, q.bits, q.zero, q.denorm };
+    return rsqrt_newton(a, rsqrtss_emulated(a, tb));
+}
+__device__ __forceinline__ f3 normalize(f3 a, const Rsq& q) { return scale(a, rsqrt_ref(dot(a, a), q)); }
+
+struct Rng {
+    uint64_t* base;  // lane-offset base of this wave slot's state, stride 64 words
+    int       cur;   // generation buffer being consumed
+    int       idx;   // next word in it
+    int       ready; // other buffer already holds the next generation
+    uint32_t  draws;
+};
+
+__device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_N * 64; }
+
+// B = twist(A) without modifying A (in-place MT19937-64 twist split over two buffers).
+__device__ __noinline__ void mt_twist_into(const uint64_t* A, uint64_t* B)
+{
+    uint64_t ak = A[0];
+#pragma unroll 4
+    for (int k = 0; k < MT_N - MT_M; ++k) {
+        const uint64_t ak1 = A[(k + 1) * 64];
+        B[k * 64]          = A[(k + MT_M) * 64] ^ mt_mix(ak, ak1);
+        ak                 = ak1;
+    }
+#pragma unroll 4
+    for (int k = MT_N - MT_M; k < MT_N - 1; ++k) {
+        const uint64_t ak1 = A[(k + 1) * 64];
+        B[k * 64]          = B[(k - (MT_N - MT_M)) * 64] ^ mt_mix(ak, ak1);
+        ak                 = ak1;
+    }
+    B[(MT_N - 1) * 64] = B[(MT_M - 1) * 64] ^ mt_mix(ak, B[0]);
+}
+
+__device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
+{
+    uint64_t* b = mt_buf(r, 0);
+    uint64_t  x = (uint64_t)seed;
+    b[0]        = x;
+    for (int i = 1; i < MT_N; ++i) {
+        x          = mt_seed_next(x, (uint64_t)i);
+        b[i * 64]  = x;
+    }
+    r.cur   = 0;
+    r.idx   = MT_N; // std::mt19937_64 starts with _M_p = n: first draw twists
+    r.ready = 0;
+    r.draws = 0;
+}
+
+// Twist ahead at a wave-synchronous point (sample / bounce start) so lanes twist together.
+__device__ __forceinline__ void rng_prepare(Rng& r)
+{
+    if (!r.ready && r.idx >= 96) {
+        mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
+        r.ready = 1;
+    }
+}
+
+__device__ __forceinline__ uint64_t rng_raw(Rng& r)
+{
+    if (r.idx >= MT_N) {
+        if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
+        r.cur ^= 1;
+        r.idx   = 0;
+        r.ready = 0;
+    }
+    const uint64_t w = mt_buf(r, r.cur)[(size_t)r.idx * 64];
+    ++r.idx;
+    ++r.draws;
+    return mt_temper(w);
+}
+
+// IncoherentSampler::get_next_1D / get_next_2D (math/Sampler.h:110-118)
+__device__ __forceinline__ float next1D(Rng& r) { return canonical_from_u64(rng_raw(r)); }
+struct P2 {
+    float x, y;
+};
+__device__ __forceinline__ P2 next2D(Rng& r)
+{
+    P2 p;
+    p.x = next1D(r); // braced-init-list: left-to-right
+    p.y = next1D(r);
+    return p;
+}
+
+// ============================================================================ rays & hits
+struct Ray {
+    f3 o, d;
+};
+__device__ __forceinline__ f3 ray_at(const Ray& r, float t) { return add(r.o, scale(r.d, t)); } // math/Ray.h:180
+
+// math/Ray.h:201
+__device__ __forceinline__ float ray_offset(float cos_d) { return (cos_d == 0.0f) ? k_ray_epsilon : k_ray_epsilon / cos_d; }
+__device__ __forceinline__ float ray_offset(f3 n, f3 d) { return ray_offset(abs_f(dot(n, d))); }
+
+// math/BBox.h:254 intersect_p(BBox, Ray, RayLimits)
+__device__ __forceinline__ bool box_hit(const Node& n, const Ray& r, const f3& inv, float tmin, float tmax)
+{
+    float t0 = tmin, t1 = tmax;
+    {
+        float tn = (n.lo[0] - r.o.x) * inv.x, tf = (n.hi[0] - r.o.x) * inv.x;
+        if (tn > tf) { const float s = tn; tn = tf; tf = s; }
+        t0 = std_max(tn, t0);
+        t1 = std_min(tf, t1);
+        if (t0 > t1) return false;
+    }
+    {
+        float tn = (n.lo[1] - r.o.y) * inv.y, tf = (n.hi[1] - r.o.y) * inv.y;
+        if (tn > tf) { const float s = tn; tn = tf; tf = s; }
+        t0 = std_max(tn, t0);
+        t1 = std_min(tf, t1);
+        if (t0 > t1) return false;
+    }
+    {
+        float tn = (n.lo[2] - r.o.z) * inv.z, tf = (n.hi[2] - r.o.z) * inv.z;
+        if (tn > tf) { const float s = tn; tn = tf; tf = s; }
+        t0 = std_max(tn, t0);
+        t1 = std_min(tf, t1);
+        if (t0 > t1) return false;
+    }
+    return true;
+}
+
+// shapes/Triangle.h:97 intersect_impl -- returns t, beta, gamma
+__device__ __forceinline__ bool tri_hit(const float4& q0, const float4& q1, const float4& q2, const Ray& ray, float tmin,
+                                        float tmax, float& t_out, float& beta_out, float& gamma_out)
+{
+    const float A = q0.x - q1.x, B = q0.y - q1.y, C = q0.z - q1.z;
+    const float D = q0.x - q2.x, E = q0.y - q2.y, F = q0.z - q2.z;
+    const float G = ray.d.x, H = ray.d.y, I = ray.d.z;
+    const float J = q0.x - ray.o.x, K = q0.y - ray.o.y, L = q0.z - ray.o.z;
+    const float EIHF  = fma_f(E, I, -(H * F));
+    const float GFDI  = fma_f(G, F, -(D * I));
+    const float DHEG  = fma_f(D, H, -(E * G));
+    const float denom = fma_f(A, EIHF, fma_f(B, GFDI, C * DHEG));
+    if (denom == 0) return false;
+    const float beta = fma_f(J, EIHF, fma_f(K, GFDI, L * DHEG)) / denom;
+    if (beta <= 0.0f || beta >= 1.0f) return false;
+    const float AKJB  = fma_f(A, K, -(J * B));
+    const float JCAL  = fma_f(J, C, -(A * L));
+    const float BLKC  = fma_f(B, L, -(K * C));
+    const float gamma = fma_f(I, AKJB, fma_f(H, JCAL, G * BLKC)) / denom;
+    if (gamma <= 0.0f || beta + gamma >= 1.0f) return false;
+    const float t = -fma_f(F, AKJB, fma_f(E, JCAL, D * BLKC)) / denom;
+    if (t < tmin || t > tmax) return false;
+    t_out     = t;
+    beta_out  = beta;
+    gamma_out = gamma;
+    return true;
+}
+
+// shapes/Sphere.h:295 intersect_impl (t only; normal derived at the end)
+__device__ __forceinline__ bool sphere_t(const aff& w2o, const Ray& ray, float tmin, float tmax, float& t_out)
+{
+    const f3    o    = xfm_point(w2o, ray.o);
+    const f3    d    = xfm_vector(w2o, ray.d);
+    const float a    = dot(d, d);
+    const float b    = 2.0f * dot(d, o);
+    const float c    = dot(o, o) - 1.0f * 1.0f;
+    float       disc = b * b - 4.0f * a * c;
+    if (disc > 0.0f) {
+        disc    = sqrt_f(disc);
+        float t = (-b - disc) / (2.0f * a);
+        if (t < tmin) t = (-b + disc) / (2.0f * a);
+        if (t < tmin || t > tmax) return false;
+        t_out = t;
+        return true;
+    }
+    return false;
+}
+
+// shapes/Plane.h:391 intersect_impl (t only)
+__device__ __forceinline__ bool plane_t(const aff& w2o, const Ray& ray, float tmin, float tmax, float& t_out)
+{
+    const f3 d = xfm_vector(w2o, ray.d);
+    if (d.y == 0.0f) return false;
+    const f3    o = xfm_point(w2o, ray.o);
+    const float t = -o.y / d.y;
+    if (t < tmin || t > tmax) return false;
+    t_out = t;
+    return true;
+}
+
+struct Hit {
+    float    t;
+    uint32_t code; // kind << 30 | index ; 0xffffffff = none
+    float    beta, gamma;
+};
+
+constexpr uint32_t KIND_TRI = 0u, KIND_SPHERE = 1u, KIND_PLANE = 2u;
+
+struct Isect {
+    float t;
+    f3    n, p;
+    int   material;
+};
+
+// Shape-specific surface data for the final closest hit (identical arithmetic to the reference,
+// which computes it for every accepted candidate).
+__device__ __forceinline__ Isect finish_hit(const Scene& sc, const Hit& h, const Ray& ray, const Rsq& q)
+{
+    Isect          is;
+    const uint32_t kind = h.code >> CODE_SHIFT;
+    const uint32_t id   = h.code & CODE_MASK;
+    is.t = h.t;
+    is.p = ray_at(ray, h.t);
+    if (kind == KIND_TRI) {
+        const uint32_t i0 = sc.indices[3 * id], i1 = sc.indices[3 * id + 1], i2 = sc.indices[3 * id + 2];
+        const f3 n0 = mk(sc.normals[3 * i0], sc.normals[3 * i0 + 1], sc.normals[3 * i0 + 2]);
+        const f3 n1 = mk(sc.normals[3 * i1], sc.normals[3 * i1 + 1], sc.normals[3 * i1 + 2]);
+        const f3 n2 = mk(sc.normals[3 * i2], sc.normals[3 * i2 + 1], sc.normals[3 * i2 + 2]);
+        const float alpha = 1.0f - h.beta - h.gamma;
+        is.n        = normalize(madd(alpha, n0, madd(h.beta, n1, scale(h.gamma, n2))), q);
+        is.material = sc.tri_material[id];
+    } else if (kind == KIND_SPHERE) {
+        const Shape& s = sc.shapes[id];
+        const f3     o = xfm_point(s.w2o, ray.o);
+        const f3     d = xfm_vector(s.w2o, ray.d);
+        const f3     nl = divs(madd(h.t, d, o), 1.0f);
+        is.n        = normalize(xfm_vector(s.nrm, nl), q);
+        is.material = s.material;
+    } else {
+        const Shape& s = sc.shapes[id];
+        is.n        = xfm_vector(s.nrm, mk(0.0f, 1.0f, 0.0f));
+        is.material = s.material;
+    }
+    return is;
+}
+
+// Test one primitive code against the ray (closest-hit semantics: t <= tmax accepted).
+__device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h)
+{
+    const uint32_t code = sc.slot_code[slot];
+    const uint32_t kind = code >> CODE_SHIFT;
+    if (kind == KIND_TRI) {
+        const float4 q0 = sc.slot_tri[3 * slot], q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
+        float t, be, ga;
+        if (tri_hit(q0, q1, q2, ray, tmin, h.t, t, be, ga)) {
+            h.t = t; h.code = code; h.beta = be; h.gamma = ga;
+            return true;
+        }
+        return false;
+    }
+    const Shape& s = sc.shapes[code & CODE_MASK];
+    float        t;
+    const bool   hit = (kind == KIND_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
+    if (hit) { h.t = t; h.code = code; }
+    return hit;
+}
+
+__device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, float tmax)
+{
+    const uint32_t code = sc.slot_code[slot];
+    const uint32_t kind = code >> CODE_SHIFT;
+    if (kind == KIND_TRI) {
+        const float4 q0 = sc.slot_tri[3 * slot], q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
+        float t, be, ga;
+        return tri_hit(q0, q1, q2, ray, tmin, tmax, t, be, ga);
+    }
+    const Shape& s = sc.shapes[code & CODE_MASK];
+    float        t;
+    return (kind == KIND_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t);
+}
+
+// LDS traversal stack: entry e of lane l at stack[e * 64 + l].  Entries are nodes whose box
+// test is still pending, popped child-0-first: the visiting order of the reference's recursion
+// (shapes/BVHAccelerator.h:62-77) with each box tested against the limits current at that time.
+struct Stack {
+    uint32_t* s;
+    int       lane;
+};
+
+// Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
+__device__ __noinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    Hit h;
+    h.t    = tmax;
+    h.code = 0xffffffffu;
+    for (int i = 0; i < sc.n_unbounded; ++i) {
+        const int    sid = sc.unbounded[i];
+        const Shape& s   = sc.shapes[sid];
+        float        t;
+        const bool   hit = (s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
+        if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
+    }
+    if (sc.n_nodes == 0) return h;
+    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp  = 0;
+    uint32_t cur = 0;      // root: no box test
+    bool     test_box = false;
+    while (true) {
+        const Node n = sc.nodes[cur];
+        if (!test_box || box_hit(n, ray, inv, tmin, h.t)) {
+            if (n.b & LEAF_BIT) {
+                const uint32_t cnt = n.b & ~LEAF_BIT;
+                for (uint32_t k = 0; k < cnt; ++k) prim_closest(sc, n.a + k, ray, tmin, h);
+            } else {
+                st.s[sp * 64 + st.lane] = n.b; // child 1 deferred
+                ++sp;
+                cur      = n.a;                 // child 0 next
+                test_box = true;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur      = st.s[sp * 64 + st.lane];
+        test_box = true;
+    }
+    return h;
+}
+
+// any-hit over the geometry accelerator (ListAccelerator::intersect_p_impl)
+__device__ __noinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    for (int i = 0; i < sc.n_unbounded; ++i) {
+        const Shape& s = sc.shapes[sc.unbounded[i]];
+        float        t;
+        if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
+    }
+    if (sc.n_nodes == 0) return false;
+    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp  = 0;
+    uint32_t cur = 0;
+    bool     test_box = false;
+    while (true) {
+        const Node n = sc.nodes[cur];
+        if (!test_box || box_hit(n, ray, inv, tmin, tmax)) {
+            if (n.b & LEAF_BIT) {
+                const uint32_t cnt = n.b & ~LEAF_BIT;
+                for (uint32_t k = 0; k < cnt; ++k)
+                    if (prim_any(sc, n.a + k, ray, tmin, tmax)) return true;
+            } else {
+                st.s[sp * 64 + st.lane] = n.b;
+                ++sp;
+                cur      = n.a;
+                test_box = true;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur      = st.s[sp * 64 + st.lane];
+        test_box = true;
+    }
+    return false;
+}
+
+// ------------------------------------------------------------------------------ lights
+struct LightHit {
+    bool  hit;
+    float t;
+    rgb   L;
+};
+
+// Scene::intersect_lights (base/Scene.h:69): ListAccelerator{environment..., BVH(sphere lights)}
+__device__ __noinline__ LightHit scene_intersect_lights(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    LightHit lh;
+    lh.hit = false;
+    lh.t   = tmax;
+    for (int i = 0; i < sc.n_unbounded_lights; ++i) {
+        const Light& l = sc.lights[sc.unbounded_lights[i]];
+        // EnvironmentLight::intersect_lights_impl (Lights/Light.h:242)
+        if (!(lh.t < k_infinite)) {
+            lh.hit = true;
+            lh.t   = k_infinite;
+            lh.L   = l.radiance;
+        }
+    }
+    if (sc.n_light_nodes == 0) return lh;
+    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp  = 0;
+    uint32_t cur = 0;
+    bool     test_box = false;
+    while (true) {
+        const Node n = sc.light_nodes[cur];
+        if (!test_box || box_hit(n, ray, inv, tmin, lh.t)) {
+            if (n.b & LEAF_BIT) {
+                const uint32_t cnt = n.b & ~LEAF_BIT;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const Light& l = sc.lights[sc.light_slot[n.a + k]];
+                    float        t;
+                    if (sphere_t(l.w2o, ray, tmin, lh.t, t)) {
+                        lh.hit = true;
+                        lh.t   = t;
+                        lh.L   = l.radiance;
+                    }
+                }
+            } else {
+                st.s[sp * 64 + st.lane] = n.b;
+                ++sp;
+                cur      = n.a;
+                test_box = true;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur      = st.s[sp * 64 + st.lane];
+        test_box = true;
+    }
+    return lh;
+}
+
+__device__ __noinline__ bool lights_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    if (sc.n_light_nodes == 0) return false; // environment lights never occlude
+    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp  = 0;
+    uint32_t cur = 0;
+    bool     test_box = false;
+    while (true) {
+        const Node n = sc.light_nodes[cur];
+        if (!test_box || box_hit(n, ray, inv, tmin, tmax)) {
+            if (n.b & LEAF_BIT) {
+                const uint32_t cnt = n.b & ~LEAF_BIT;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const Light& l = sc.lights[sc.light_slot[n.a + k]];
+                    float        t;
+                    if (sphere_t(l.w2o, ray, tmin, tmax, t)) return true;
+                }
+            } else {
+                st.s[sp * 64 + st.lane] = n.b;
+                ++sp;
+                cur      = n.a;
+                test_box = true;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur      = st.s[sp * 64 + st.lane];
+        test_box = true;
+    }
+    return false;
+}
+
+// Scene::intersect_p (base/Scene.h:79)
+__device__ __forceinline__ bool scene_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    return geometry_any(sc, ray, tmin, tmax, st) || lights_any(sc, ray, tmin, tmax, st);
+}
+
+// ------------------------------------------------------------------------------ sampling
+// math/Sampling.h:222
+__device__ __forceinline__ f3 sample_uniform_sphere(P2 u)
+{
+    const float z   = 1.0f - 2.0f * u.x;
+    const float r   = sqrt_f(std_max(0.0f, 1.0f - z * z));
+    const float phi = (float)(2.0 * (double)k_pi * (double)u.y);
+    return mk(r * lm_cosf(phi), r * lm_sinf(phi), z);
+}
+// math/Sampling.h:235
+__device__ __forceinline__ f3 sample_uniform_hemisphere(P2 u)
+{
+    const float y   = u.x;
+    const float r   = sqrt_f(std_max(0.0f, 1.0f - y * y));
+    const float phi = 2.0f * k_pi * u.y;
+    return mk(r * lm_cosf(phi), y, r * lm_sinf(phi));
+}
+// math/Sampling.cpp:304
+__device__ __forceinline__ P2 concentric_disk(P2 u)
+{
+    constexpr float pi_over_4 = k_pi / 4.0f;
+    constexpr float pi_over_2 = k_pi / 2.0f;
+    const float     ox = 2.0f * u.x - 1.0f;
+    const float     oy = 2.0f * u.y - 1.0f;
+    P2              r;
+    if (ox == 0.0f && oy == 0.0f) { r.x = 0.0f; r.y = 0.0f; return r; }
+    float theta, rad;
+    if (abs_f(ox) > abs_f(oy)) { rad = ox; theta = pi_over_4 * (oy / ox); }
+    else { rad = oy; theta = pi_over_2 - pi_over_4 * (ox / oy); }
+    r.x = rad * lm_cosf(theta);
+    r.y = rad * lm_sinf(theta);
+    return r;
+}
+__device__ __forceinline__ f3 sample_cosine_hemisphere(P2 u)
+{
+    const P2    d = concentric_disk(u);
+    const float y = sqrt_f(std_max(0.0f, 1.0f - d.x * d.x - d.y * d.y));
+    return mk(d.x, y, d.y);
+}
+constexpr float k_uniform_sphere_pdf     = 1.0f / (4.0f * k_pi);
+constexpr float k_uniform_hemisphere_pdf = 1.0f / (2.0f * k_pi);
+
+// math/ONB.h
+struct Onb {
+    f3 u, v, w;
+};
+__device__ __forceinline__ Onb onb_from_v(f3 n, const Rsq& q)
+{
+    const f3    v    = normalize(n, q);
+    const float sign = copysign_f(1.0f, v.z);
+    const float a    = -1.0f / (sign + v.z);
+    const float b    = v.x * v.y * a;
+    const f3    b1   = mk(1.0f + sign * v.x * v.x * a, sign * b, -sign * v.x);
+    const f3    b2   = mk(b, sign + v.y * v.y * a, -v.y);
+    Onb         o;
+    o.u = b2; // [w, u] = create(v)
+    o.v = v;
+    o.w = b1;
+    return o;
+}
+__device__ __forceinline__ f3 to_world(const Onb& o, f3 a) { return add(add(scale(a.x, o.u), scale(a.y, o.v)), scale(a.z, o.w)); }
+__device__ __forceinline__ f3 to_onb(const Onb& o, f3 a) { return mk(dot(a, o.u), dot(a, o.v), dot(a, o.w)); }
+
+// ------------------------------------------------------------------------------ materials
+struct MSample {
+    rgb   color;
+    f3    dir;
+    float pdf;
+    int   props;
+};
+constexpr int PROP_DIFFUSE = 1, PROP_GLOSSY = 2, PROP_SPECULAR = 4, PROP_REFLECTIVE = 8;
+
+__device__ __forceinline__ float cos2_theta(f3 w) { return w.y * w.y; }
+__device__ __forceinline__ float sin2_theta(f3 w) { return std_max(0.0f, 1.0f - cos2_theta(w)); }
+__device__ __forceinline__ float sin_theta(f3 w) { return sqrt_f(sin2_theta(w)); }
+__device__ __forceinline__ float tan_theta(f3 w) { return sin_theta(w) / w.y; }
+__device__ __forceinline__ float tan2_theta(f3 w) { return sin2_theta(w) / cos2_theta(w); }
+__device__ __forceinline__ float cos_phi(f3 w)
+{
+    const float st = sin_theta(w);
+    return (st == 0.0f) ? 1.0f : std_clamp(w.x / st, -1.0f, 1.0f);
+}
+__device__ __forceinline__ float sin_phi(f3 w)
+{
+    const float st = sin_theta(w);
+    return (st == 0.0f) ? 1.0f : std_clamp(w.z / st, -1.0f, 1.0f);
+}
+__device__ __forceinline__ bool same_hemisphere(f3 a, f3 b) { return a.y * b.y > 0.0f; }
+
+// materials/Material.h:114
+__device__ __forceinline__ float fresnel_dielectric(float cos_i, float eta_i, float eta_t)
+{
+    cos_i = std_clamp(cos_i, -1.0f, 1.0f);
+    if (!(cos_i > 0.0f)) {
+        const float s = eta_i; eta_i = eta_t; eta_t = s;
+        cos_i = abs_f(cos_i);
+    }
+    const float sin_i = sqrt_f(std_max(0.0f, 1.0f - cos_i * cos_i));
+    const float sin_t = eta_i / eta_t * sin_i;
+    if (sin_t >= 1) return 1.0f;
+    const float cos_t = sqrt_f(std_max(0.0f, 1.0f - sin_t * sin_t));
+    const float parl  = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
+    const float perp  = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
+    return (parl * parl + perp * perp) / 2.0f;
+}
+
+// math/Math.h:230 erfinv
+__device__ __forceinline__ float erfinv(float a)
+{
+    float       p;
+    const float t = lm_logf(fma_f(a, 0.0f - a, 1.0f));
+    if (abs_f(t) > 6.125f) {
+        p = 3.03697567e-10f;
+        p = fma_f(p, t, 2.93243101e-8f);
+        p = fma_f(p, t, 1.22150334e-6f);
+        p = fma_f(p, t, 2.84108955e-5f);
+        p = fma_f(p, t, 3.93552968e-4f);
+        p = fma_f(p, t, 3.02698812e-3f);
+        p = fma_f(p, t, 4.83185798e-3f);
+        p = fma_f(p, t, -2.64646143e-1f);
+        p = fma_f(p, t, 8.40016484e-1f);
+    } else {
+        p = 5.43877832e-9f;
+        p = fma_f(p, t, 1.43285448e-7f);
+        p = fma_f(p, t, 1.22774793e-6f);
+        p = fma_f(p, t, 1.12963626e-7f);
+        p = fma_f(p, t, -5.61530760e-5f);
+        p = fma_f(p, t, -1.47697632e-4f);
+        p = fma_f(p, t, 2.31468678e-3f);
+        p = fma_f(p, t, 1.15392581e-2f);
+        p = fma_f(p, t, -2.32015476e-1f);
+        p = fma_f(p, t, 8.86226892e-1f);
+    }
+    return a * p;
+}
+
+// materials/Material.cpp:14 beckmann_sample11
+__device__ __noinline__ P2 beckmann_sample11(float cos_theta_i, float U1, float U2)
+{
+    P2 s;
+    if (cos_theta_i > .9999f) {
+        const float r  = sqrt_f(-lm_logf(1.0f - U1));
+        const float sp = lm_sinf(2.0f * k_pi * U2);
+        const float cp = lm_cosf(2.0f * k_pi * U2);
+        s.x = r * cp;
+        s.y = r * sp;
+        return s;
+    }
+    const float sin_theta_i = sqrt_f(std_max(0.0f, 1.0f - cos_theta_i * cos_theta_i));
+    const float tan_theta_i = sin_theta_i / cos_theta_i;
+    const float cot_theta_i = 1.0f / tan_theta_i;
+    float       a           = -1.0f;
+    float       c           = lm_erff(cot_theta_i);
+    const float sample_x    = std_max(U1, 1e-6f);
+    const float theta_i     = lm_acosf(cos_theta_i);
+    const float fit         = 1.0f + theta_i * (-0.876f + theta_i * (0.4265f - 0.0594f * theta_i));
+    float       b           = c - (1.0f + c) * lm_powf(1.0f - sample_x, fit);
+    const float sqrt_pi_inv = 1.0f / sqrt_f(k_pi);
+    const float normalization =
+        1.0f / (1.0f + c + sqrt_pi_inv * tan_theta_i * lm_expf(-cot_theta_i * cot_theta_i));
+    for (int it = 0; it < 9; ++it) {
+        if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+        const float inv_erf = erfinv(b);
+        const float value =
+            normalization * (1.0f + b + sqrt_pi_inv * tan_theta_i * lm_expf(-inv_erf * inv_erf)) - sample_x;
+        const float derivative = normalization * (1.0f - inv_erf * tan_theta_i);
+        if (abs_f(value) < 1e-5f) break;
+        if (value > 0) c = b;
+        else a = b;
+        b -= value / derivative;
+    }
+    s.x = erfinv(b);
+    s.y = erfinv(2.0f * std_max(U2, 1e-6f) - 1.0f);
+    return s;
+}
+
+// materials/Material.cpp:89 beckmann_sample
+__device__ __forceinline__ f3 beckmann_sample(f3 wi, float ax, float ay, float U1, float U2, const Rsq& q)
+{
+    const f3 st = normalize(mk(ax * wi.x, wi.y, ay * wi.z), q);
+    P2       sl = beckmann_sample11(st.y, U1, U2);
+    const float tmp = cos_phi(st) * sl.x - sin_phi(st) * sl.y;
+    sl.y            = sin_phi(st) * sl.x + cos_phi(st) * sl.y;
+    sl.x            = tmp;
+    sl.x            = ax * sl.x;
+    sl.y            = ay * sl.y;
+    return normalize(mk(-sl.x, 1.0f, -sl.y), q);
+}
+
+// BeckmannDistribution (materials/Material.h:213)
+__device__ __forceinline__ float beck_D(const Material& m, f3 wh)
+{
+    const float t2 = tan2_theta(wh);
+    if (__builtin_isinf(t2)) return 0.0f;
+    const float c4 = cos2_theta(wh) * cos2_theta(wh);
+    const float cp = cos_phi(wh), sp = sin_phi(wh);
+    return lm_expf(-t2 * ((cp * cp) / (m.alpha_x * m.alpha_x) + (sp * sp) / (m.alpha_y * m.alpha_y))) /
+           (k_pi * m.alpha_x * m.alpha_y * c4);
+}
+__device__ __forceinline__ float beck_lambda(const Material& m, f3 w)
+{
+    const float at = abs_f(tan_theta(w));
+    if (__builtin_isinf(at)) return 0.0f;
+    const float cp    = cos_phi(w), sp = sin_phi(w);
+    const float alpha = sqrt_f((cp * cp) * (m.alpha_x * m.alpha_x) + (sp * sp) * (m.alpha_y * m.alpha_y));
+    const float a     = 1.0f / (alpha * at);
+    if (a >= 1.6f) return 0.0f;
+    return (1.0f - 1.259f * a + 0.396f * (a * a)) / (3.535f * a + 2.181f * (a * a));
+}
+__device__ __forceinline__ float beck_G1(const Material& m, f3 w) { return 1.0f / (1.0f + beck_lambda(m, w)); }
+__device__ __forceinline__ float beck_G(const Material& m, f3 wo, f3 wi) { return 1.0f / (1.0f + beck_lambda(m, wo) + beck_lambda(m, wi)); }
+__device__ __forceinline__ float beck_pdf(const Material& m, f3 wo, f3 wh)
+{
+    if (m.sample_visible_area) return beck_D(m, wh) * beck_G1(m, wo) * abs_f(dot(wo, wh)) / abs_f(wo.y);
+    return beck_D(m, wh) * abs_f(wh.y);
+}
+// materials/Material.cpp:111 (visible-area branch; the parser always builds it)
+__device__ __forceinline__ f3 beck_sample_wh(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+{
+    const bool flip = wo.y < 0.0f;
+    // arguments evaluated right to left by GCC: U2 is drawn first
+    const float U2 = next1D(rng);
+    const float U1 = next1D(rng);
+    f3 wh = beckmann_sample(flip ? neg(wo) : wo, m.alpha_x, m.alpha_y, U1, U2, q);
+    if (flip) wh = neg(wh);
+    return wh;
+}
+
+// MicrofacetReflection (materials/Material.h:386)
+__device__ __forceinline__ rgb mf_eval(const Material& m, f3 wo, f3 wi, const Rsq& q)
+{
+    const float ao = abs_f(wo.y), ai = abs_f(wi.y);
+    if (ai == 0.0f || ao == 0.0f) return mkc(0, 0, 0);
+    f3 wh = add(wi, wo);
+    if (wh.x == 0.0f && wh.y == 0.0f && wh.z == 0.0f) return mkc(0, 0, 0);
+    wh            = normalize(wh, q);
+    const float f = fresnel_dielectric(dot(wi, wh), 1.0f, m.microfacet_ior);
+    return cdivs(cscale(cscale(cscale(m.microfacet_r, beck_D(m, wh)), beck_G(m, wo, wi)), f), 4.0f * ai * ao);
+}
+__device__ __forceinline__ float mf_pdf(const Material& m, f3 wo, f3 wi, const Rsq& q)
+{
+    if (!same_hemisphere(wo, wi)) return 0.0f;
+    const f3 wh = normalize(add(wo, wi), q);
+    return beck_pdf(m, wo, wh) / (4.0f * dot(wo, wh));
+}
+__device__ __noinline__ MSample mf_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+{
+    MSample r;
+    r.color = mkc(0, 0, 0);
+    r.dir   = mk(0, 0, 0);
+    r.pdf   = 0.0f;
+    r.props = 0;
+    if (wo.y == 0.0f) return r;
+    const f3    wh = beck_sample_wh(m, wo, rng, q);
+    const float dp = dot(wo, wh);
+    if (dp < 0.0f) return r;
+    // specular_reflection(wo, n) = -wo + 2 dot(wo,n) n
+    const f3 wi = add(neg(wo), scale(2.0f * dot(wo, wh), wh));
+    if (!same_hemisphere(wo, wi)) return r;
+    r.pdf   = beck_pdf(m, wo, wh) / (4.0f * dp);
+    r.color = mf_eval(m, wo, wi, q);
+    r.dir   = wi;
+    r.props = PROP_GLOSSY | PROP_REFLECTIVE;
+    return r;
+}
+// BRDF::rho_impl default (materials/Material.h:299) for the microfacet lobe
+__device__ __noinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+{
+    rgb r = mkc(0, 0, 0);
+    for (unsigned i = 0; i < 16u; ++i) {
+        const MSample s = mf_sample(m, wo, rng, q);
+        if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
+    }
+    return cdivs(r, (float)16u);
+}
+
+// OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
+__device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
+{
+    const rgb r0 = mf_rho16(m, wo, rng, q);
+    const rgb r1 = cscale(m.lambert_albedo, k_pi); // LambertianBRDF::rho_impl
+    float     sum = 0.0f;
+    w[0] = luminance(r0);
+    sum += w[0];
+    w[1] = luminance(r1);
+    sum += w[1];
+    w[0] = w[0] / sum;
+    w[1] = w[1] / sum;
+}
+__device__ __forceinline__ float lambert_only_weight(const Material& m)
+{
+    const rgb r   = cscale(m.lambert_albedo, k_pi);
+    float     sum = 0.0f;
+    float     w   = luminance(r);
+    sum += w;
+    return w / sum;
+}
+__device__ __forceinline__ float balance(float p, float inner) { return (inner == 0.0f) ? 0.0f : p / inner; }
+
+__device__ __forceinline__ MSample lambert_sample(const Material& m, Rng& rng)
+{
+    MSample r;
+    const P2 u = next2D(rng);
+    r.dir      = sample_uniform_hemisphere(u);
+    r.color    = m.lambert_albedo;
+    r.pdf      = k_uniform_hemisphere_pdf;
+    r.props    = PROP_DIFFUSE | PROP_REFLECTIVE;
+    return r;
+}
+
+// Local-space sample/eval/pdf of a non-clearcoat material (OneSampleMaterial).
+__device__ __noinline__ MSample onesample_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+{
+    if (m.kind == SP_MAT_LAMBERTIAN) return lambert_sample(m, rng);
+    float w[2];
+    glossy_weights(m, wo, rng, q, w);
+    const float u   = next1D(rng);
+    float       cdf = 0.0f;
+    int         sel = 1; // loop falls through only on NaN weights (uninitialised in the reference)
+    for (int i = 0; i < 2; ++i) {
+        if (w[i] + cdf > u) { sel = i; break; }
+        cdf += w[i];
+    }
+    MSample res = (sel == 0) ? mf_sample(m, wo, rng, q) : lambert_sample(m, rng);
+    if (res.pdf == 0.0f || cblack(res.color)) {
+        MSample z;
+        z.color = mkc(0, 0, 0); z.dir = mk(0, 0, 0); z.pdf = 0.0f; z.props = 0;
+        return z;
+    }
+    const f3 wi = res.dir;
+    rgb      values[2];
+    float    pdfs[2];
+    for (int i = 0; i < 2; ++i) {
+        if (i == sel) {
+            values[i] = res.color;
+            pdfs[i]   = res.pdf * w[i];
+        } else if (i == 0) {
+            values[i] = mf_eval(m, wo, wi, q);
+            pdfs[i]   = mf_pdf(m, wo, wi, q) * w[i];
+        } else {
+            values[i] = m.lambert_albedo;
+            pdfs[i]   = k_uniform_hemisphere_pdf * w[i];
+        }
+    }
+    const float inner = (0.0f + pdfs[0]) + pdfs[1];
+    rgb         col   = mkc(0, 0, 0);
+    float       pdf   = 0.0f;
+    for (int i = 0; i < 2; ++i) {
+        if (pdfs[i] > 0.0f) {
+            const float mw = balance(pdfs[i], inner);
+            col            = cadd(col, cscale(values[i], mw));
+            pdf += pdfs[i];
+        }
+    }
+    MSample out;
+    out.color = col;
+    out.dir   = wi;
+    out.pdf   = pdf;
+    out.props = res.props;
+    return out;
+}
+
+__device__ __noinline__ rgb onesample_eval(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
+{
+    if (m.kind == SP_MAT_LAMBERTIAN) {
+        const float w     = lambert_only_weight(m);
+        const float p     = k_uniform_hemisphere_pdf * w;
+        const float inner = 0.0f + p;
+        rgb         r     = mkc(0, 0, 0);
+        if (p > 0.0f) r = cadd(r, cscale(m.lambert_albedo, balance(p, inner)));
+        return r;
+    }
+    float w[2];
+    glossy_weights(m, wo, rng, q, w);
+    const float p0    = mf_pdf(m, wo, wi, q) * w[0];
+    const float p1    = k_uniform_hemisphere_pdf * w[1];
+    const float inner = (0.0f + p0) + p1;
+    rgb         r     = mkc(0, 0, 0);
+    if (p0 > 0.0f) r = cadd(r, cscale(mf_eval(m, wo, wi, q), balance(p0, inner)));
+    if (p1 > 0.0f) r = cadd(r, cscale(m.lambert_albedo, balance(p1, inner)));
+    return r;
+}
+
+__device__ __noinline__ float onesample_pdf(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
+{
+    if (m.kind == SP_MAT_LAMBERTIAN) {
+        const float w = lambert_only_weight(m);
+        float       p = 0.0f;
+        p += w * k_uniform_hemisphere_pdf;
+        return p;
+    }
+    float w[2];
+    glossy_weights(m, wo, rng, q, w);
+    float p = 0.0f;
+    p += w[0] * mf_pdf(m, wo, wi, q);
+    p += w[1] * k_uniform_hemisphere_pdf;
+    return p;
+}
+
+// Material::sample/eval/pdf incl. ClearcoatMaterial (materials/Material.h:461-529, 723-806)
+__device__ __forceinline__ MSample material_sample_local(const Scene& sc, int mid, f3 wo, Rng& rng, const Rsq& q)
+{
+    const Material& m = sc.materials[mid];
+    if (m.kind != SP_MAT_CLEARCOAT) return onesample_sample(m, wo, rng, q);
+    const float f = fresnel_dielectric(wo.y, 1.0f, m.coat_ior);
+    const float u = next1D(rng);
+    if (u < f) {
+        MSample s;
+        s.dir   = mk(-wo.x, wo.y, -wo.z);
+        s.color = cdivs(cscale(m.coat_color, f), abs_f(s.dir.y));
+        s.pdf   = f;
+        s.props = PROP_SPECULAR | PROP_REFLECTIVE;
+        return s;
+    }
+    MSample b = onesample_sample(sc.materials[m.base], wo, rng, q);
+    if (b.pdf == 0.0f) return b;
+    MSample s;
+    s.pdf   = (1.0f - f) * b.pdf;
+    s.color = cmul(csub(mkc(1, 1, 1), cscale(m.coat_color, f)), b.color);
+    s.dir   = b.dir;
+    s.props = b.props;
+    return s;
+}
+__device__ __forceinline__ rgb material_eval_local(const Scene& sc, int mid, f3 wo, f3 wi, Rng& rng, const Rsq& q)
+{
+    const Material& m = sc.materials[mid];
+    if (m.kind != SP_MAT_CLEARCOAT) return onesample_eval(m, wo, wi, rng, q);
+    const float f = fresnel_dielectric(wo.y, 1.0f, m.coat_ior);
+    return cscale(onesample_eval(sc.materials[m.base], wo, wi, rng, q), 1.0f - f);
+}
+__device__ __forceinline__ float material_pdf_local(const Scene& sc, int mid, f3 wo, f3 wi, Rng& rng, const Rsq& q)
+{
+    const Material& m = sc.materials[mid];
+    if (m.kind != SP_MAT_CLEARCOAT) return onesample_pdf(m, wo, wi, rng, q);
+    const float f = fresnel_dielectric(wo.y, 1.0f, m.coat_ior);
+    return (1.0f - f) * onesample_pdf(sc.materials[m.base], wo, wi, rng, q);
+}
+
+__device__ __forceinline__ MSample material_sample(const Scene& sc, int mid, f3 wo_w, f3 n, Rng& rng, const Rsq& q)
+{
+    const Onb o = onb_from_v(n, q);
+    MSample   r = material_sample_local(sc, mid, to_onb(o, wo_w), rng, q);
+    if (r.pdf == 0.0f || cblack(r.color)) return r;
+    r.dir = to_world(o, r.dir);
+    return r;
+}
+__device__ __forceinline__ rgb material_eval(const Scene& sc, int mid, f3 wo, f3 wi, f3 n, Rng& rng, const Rsq& q)
+{
+    const Onb o = onb_from_v(n, q);
+    return material_eval_local(sc, mid, to_onb(o, wo), to_onb(o, wi), rng, q);
+}
+__device__ __forceinline__ float material_pdf(const Scene& sc, int mid, f3 wo, f3 wi, f3 n, Rng& rng, const Rsq& q)
+{
+    const Onb o = onb_from_v(n, q);
+    return material_pdf_local(sc, mid, to_onb(o, wo), to_onb(o, wi), rng, q);
+}
+
+// ------------------------------------------------------------------------------ light sampling
+struct LSample {
+    rgb   L;
+    float pdf;
+    Ray   ray;
+    float tmin, tmax;
+};
+
+// Sphere::pdf (shapes/Sphere.h:271)
+__device__ __forceinline__ float sphere_pdf(const Light& l, f3 observer_world)
+{
+    const f3    obs = xfm_point(l.w2o, observer_world);
+    const float sqr = dot(obs, obs);
+    if (sqr <= 1.0f) return k_uniform_sphere_pdf;
+    constexpr float sin2_1_5_deg = 0.00068523f;
+    const float     sin2_max     = 1.0f / sqr;
+    const float     cos_max      = sqrt_f(std_max(0.0f, 1.0f - sin2_max));
+    const float     omc          = (sin2_max < sin2_1_5_deg) ? sin2_max / 2.0f : 1.0f - cos_max;
+    return 1.0f / (2.0f * k_pi * omc);
+}
+
+// Light::sample (Lights/Light.h:145) for SphereLight / EnvironmentLight
+__device__ __noinline__ LSample light_sample(const Light& l, f3 obs, f3 obs_n, P2 u, const Rsq& q)
+{
+    LSample s;
+    f3      wi;
+    float   pdf, max_dist;
+    if (l.kind == SP_LIGHT_SPHERE) {
+        // Sphere::sample(observer, u) (shapes/Sphere.h:245)
+        const f3 lo = xfm_point(l.w2o, obs);
+        f3       local;
+        if (dot(lo, lo) <= 1.0f) {
+            local = sample_uniform_sphere(u);
+        } else {
+            const f3  smp = sample_cosine_hemisphere(u);
+            const Onb o   = onb_from_v(lo, q);
+            local         = to_world(o, smp);
+        }
+        const f3 sp_w = xfm_point(l.o2w, local);
+        const f3 sn_w = xfm_vector(l.nrm, local);
+        // ObjectLight::sample_impl (Lights/Light.h:188)
+        const f3 to_sample = sub(sp_w, obs);
+        wi                 = normalize(to_sample, q);
+        pdf                = sphere_pdf(l, obs);
+        max_dist           = length(to_sample) - ray_offset(sn_w, neg(wi));
+    } else {
+        // EnvironmentLight::light_sample (Lights/Light.h:265)
+        wi       = sample_uniform_sphere(u);
+        pdf      = k_uniform_sphere_pdf;
+        max_dist = k_infinite;
+    }
+    s.L     = l.radiance;
+    s.pdf   = pdf;
+    s.tmin  = ray_offset(obs_n, wi);
+    s.tmax  = max_dist;
+    s.ray.o = obs;
+    s.ray.d = wi;
+    return s;
+}
+__device__ __forceinline__ float light_pdf(const Light& l, f3 obs, f3 /*wi*/)
+{
+    return (l.kind == SP_LIGHT_SPHERE) ? sphere_pdf(l, obs) : k_uniform_sphere_pdf;
+}
+
+// ============================================================================ integrators
+struct Ctx {
+    const Scene& sc;
+    Rng&         rng;
+    const Rsq&   q;
+    Stack        st;
+    uint32_t     rays, shadow;
+};
+
+__device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float tmax)
+{
+    ++c.shadow;
+    ++c.rays;
+    return scene_any(c.sc, r, tmin, tmax, c.st);
+}
+
+// Shared "primary" query of every integrator: intersect_lights then intersect.
+struct Query {
+    LightHit lh;
+    bool     geom;
+    Isect    is;
+};
+__device__ __forceinline__ Query trace(Ctx& c, const Ray& ray, float tmin, float tmax)
+{
+    Query qr;
+    ++c.rays;
+    qr.lh = scene_intersect_lights(c.sc, ray, tmin, tmax, c.st);
+    if (qr.lh.hit) tmax = qr.lh.t;
+    const Hit h = scene_intersect(c.sc, ray, tmin, tmax, c.st);
+    qr.geom     = (h.code != 0xffffffffu);
+    if (qr.geom) qr.is = finish_hit(c.sc, h, ray, c.q);
+    return qr;
+}
+
+// DirectLightingIntegrator::do_integrate (Integrators/Integrator.cpp:277) -- also the NEE part
+// of WhittedIntegrator.
+__device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
+{
+    rgb L = mkc(0, 0, 0);
+    for (int li = 0; li < c.sc.n_lights; ++li) {
+        const Light&  l  = c.sc.lights[li];
+        const LSample ls = light_sample(l, is.p, is.n, next2D(c.rng), c.q);
+        if (ls.pdf == 0.0f || cblack(ls.L)) continue;
+        const f3  wi = ls.ray.d;
+        const rgb f  = material_eval(c.sc, is.material, wo, wi, is.n, c.rng, c.q);
+        if (!cblack(f) && !occluded(c, ls.ray, ls.tmin, ls.tmax))
+            L = cadd(L, cdivs(cscale(cmul(f, ls.L), abs_f(dot(wi, is.n))), ls.pdf));
+    }
+    return L;
+}
+
+__device__ __noinline__ rgb integrate_direct(Ctx& c, Ray ray)
+{
+    rgb L = mkc(0, 0, 0);
+    if (0 >= c.sc.max_depth) return L;
+    const Query qr = trace(c, ray, k_ray_epsilon, k_infinite);
+    if (qr.geom) {
+        L = direct_nee(c, qr.is, neg(ray.d));
+    } else if (qr.lh.hit) {
+        L = cadd(L, cmul(mkc(1, 1, 1), qr.lh.L));
+    }
+    return L;
+}
+
+// BruteForceIntegratorIterative(RR) (Integrators/Integrator.cpp:160 / 211)
+template <bool RR>
+__device__ __noinline__ rgb integrate_iterative(Ctx& c, Ray ray)
+{
+    rgb   throughput = mkc(1, 1, 1);
+    rgb   L          = mkc(0, 0, 0);
+    float tmin = k_ray_epsilon, tmax = k_infinite;
+    constexpr float rr_cut = 0.1f;
+    for (int depth = 0; depth < c.sc.max_depth; ++depth) {
+        rng_prepare(c.rng);
+        const Query qr = trace(c, ray, tmin, tmax);
+        if (qr.geom) {
+            const f3      wo = neg(ray.d);
+            const f3      n  = qr.is.n;
+            const MSample s  = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
+            if (s.pdf == 0.0f || cblack(s.color)) break;
+            const f3    wi     = s.dir;
+            const float cosine = abs_f(dot(wi, n));
+            throughput         = cmul(throughput, cdivs(cscale(s.color, cosine), s.pdf));
+            if (RR && depth >= c.sc.rr_depth) {
+                const float lum = luminance(throughput);
+                if (lum < rr_cut) {
+                    const float qv = std_max(0.05f, lum / rr_cut);
+                    if (next1D(c.rng) < qv) throughput = cdivs(throughput, qv);
+                    else break;
+                }
+            }
+            ray.o = ray_at(ray, qr.is.t);
+            ray.d = wi;
+            tmin  = ray_offset(cosine);
+            tmax  = k_infinite;
+        } else if (qr.lh.hit) {
+            L = cadd(L, cmul(throughput, qr.lh.L));
+            break;
+        } else {
+            break;
+        }
+    }
+    return L;
+}
+
+// BruteForceIntegrator (recursive, Integrators/Integrator.cpp:116), unrolled: the recursion's
+// product ((L_{k+1} * cos_k) * color_k) / pdf_k is folded back from the deepest level.
+constexpr int MAX_RECURSION = 32;
+__device__ __noinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
+{
+    float cosv[MAX_RECURSION];
+    rgb   colv[MAX_RECURSION];
+    float pdfv[MAX_RECURSION];
+    int   depth = 0;
+    rgb   Lend  = mkc(0, 0, 0);
+    const int maxd = c.sc.max_depth < MAX_RECURSION ? c.sc.max_depth : MAX_RECURSION;
+    while (true) {
+        if (depth >= maxd) { Lend = mkc(0, 0, 0); break; }
+        rng_prepare(c.rng);
+        const Query qr = trace(c, ray, k_ray_epsilon, k_infinite);
+        if (qr.geom) {
+            const f3      wo = neg(ray.d);
+            const f3      n  = qr.is.n;
+            const MSample s  = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
+            if (s.pdf == 0.0f || cblack(s.color)) { Lend = mkc(0, 0, 0); break; }
+            cosv[depth] = dot(s.dir, n);
+            colv[depth] = s.color;
+            pdfv[depth] = s.pdf;
+            ray.o       = ray_at(ray, qr.is.t);
+            ray.d       = s.dir;
+            ++depth;
+        } else if (qr.lh.hit) {
+            Lend = qr.lh.L;
+            break;
+        } else {
+            Lend = mkc(0, 0, 0);
+            break;
+        }
+    }
+    for (int k = depth - 1; k >= 0; --k) Lend = cdivs(cmul(cscale(Lend, cosv[k]), colv[k]), pdfv[k]);
+    return Lend;
+}
+
+// WhittedIntegrator (Integrators/Integrator.cpp:323): NEE at every hit, recursion on specular.
+// L_k += do_integrate(child) folds right-nested: L_0 + (L_1 + (L_2 + ...)).
+__device__ __noinline__ rgb integrate_whitted(Ctx& c, Ray ray)
+{
+    rgb       Lv[MAX_RECURSION + 1];
+    int       depth = 0;
+    const int maxd  = c.sc.max_depth < MAX_RECURSION ? c.sc.max_depth : MAX_RECURSION;
+    while (true) {
+        rgb L = mkc(0, 0, 0);
+        if (depth >= maxd) { Lv[depth] = L; break; }
+        rng_prepare(c.rng);
+        const Query qr   = trace(c, ray, k_ray_epsilon, k_infinite);
+        bool        more = false;
+        if (qr.geom) {
+            const f3 wo = neg(ray.d);
+            L           = direct_nee(c, qr.is, wo);
+            if (depth < c.sc.max_depth) {
+                const MSample s = material_sample(c.sc, qr.is.material, wo, qr.is.n, c.rng, c.q);
+                if (s.props & PROP_SPECULAR) {
+                    ray.o = qr.is.p;
+                    ray.d = s.dir;
+                    more  = true;
+                }
+            }
+        } else if (qr.lh.hit) {
+            L = cadd(L, cmul(mkc(1, 1, 1), qr.lh.L));
+        }
+        Lv[depth] = L;
+        if (!more) break;
+        ++depth;
+    }
+    rgb acc = Lv[depth];
+    for (int k = depth - 1; k >= 0; --k) acc = cadd(Lv[k], acc);
+    return acc;
+}
+
+// estimate_direct_mis (Integrators/Integrator.cpp:486)
+__device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p, f3 n, f3 wo, int mid)
+{
+    rgb           Lr = mkc(0, 0, 0);
+    const LSample ls = light_sample(l, p, n, next2D(c.rng), c.q);
+    if (ls.pdf == 0.0f || cblack(ls.L)) return Lr;
+    if (occluded(c, ls.ray, ls.tmin, ls.tmax)) return Lr;
+    const f3  wi = ls.ray.d;
+    const rgb be = material_eval(c.sc, mid, wo, wi, n, c.rng, c.q);
+    if (!cblack(be)) {
+        const float bp = material_pdf(c.sc, mid, wo, wi, n, c.rng, c.q);
+        if (bp > 0.0f) {
+            const float w = balance(ls.pdf, ls.pdf + bp);
+            Lr            = cadd(Lr, cscale(cmul(be, ls.L), abs_f(dot(wi, n)) * w / ls.pdf));
+        }
+    }
+    const MSample ms = material_sample(c.sc, mid, wo, n, c.rng, c.q);
+    if (ms.pdf == 0.0f || cblack(ms.color)) return Lr;
+    const float lp = light_pdf(l, p, ms.dir);
+    if (lp == 0.0f) return Lr;
+    const float w = balance(ms.pdf, ms.pdf + lp);
+    Ray         mr;
+    mr.o             = p;
+    mr.d             = ms.dir;
+    const float mmin = ray_offset(n, ms.dir);
+    ++c.rays;
+    const LightHit lh = scene_intersect_lights(c.sc, mr, mmin, k_infinite, c.st);
+    if (lh.hit) {
+        if (!occluded(c, mr, mmin, k_infinite))
+            Lr = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, lh.L), abs_f(dot(ms.dir, n))), w), ms.pdf));
+    }
+    return Lr;
+}
+
+// IntegratorIterativeRRNEE (Integrators/Integrator.cpp:550)
+__device__ __noinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
+{
+    rgb   throughput = mkc(1, 1, 1);
+    rgb   L          = mkc(0, 0, 0);
+    float tmin = k_ray_epsilon, tmax = k_infinite;
+    constexpr float rr_cut = 0.1f;
+    for (int depth = 0; depth < c.sc.max_depth; ++depth) {
+        rng_prepare(c.rng);
+        const Query qr = trace(c, ray, tmin, tmax);
+        if (qr.geom) {
+            const f3      wo = neg(ray.d);
+            const f3      n  = qr.is.n;
+            const MSample s  = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
+            if (s.pdf == 0.0f || cblack(s.color)) break;
+            for (int li = 0; li < c.sc.n_lights; ++li)
+                L = cadd(L, cmul(throughput, estimate_direct_mis(c, c.sc.lights[li], qr.is.p, n, wo, qr.is.material)));
+            const f3    next_o = ray_at(ray, qr.is.t);
+            const f3    wi     = s.dir;
+            const float cosine = abs_f(dot(wi, n));
+            throughput         = cmul(throughput, cdivs(cscale(s.color, cosine), s.pdf));
+            if (depth >= c.sc.rr_depth) {
+                const float lum = luminance(throughput);
+                if (lum < rr_cut) {
+                    const float qv = std_max(0.05f, lum / rr_cut);
+                    if (next1D(c.rng) < qv) throughput = cdivs(throughput, qv);
+                    else break;
+                }
+            }
+            ray.o = next_o;
+            ray.d = wi;
+            tmin  = ray_offset(cosine);
+            tmax  = k_infinite;
+        } else if (qr.lh.hit) {
+            L = cadd(L, cmul(throughput, qr.lh.L));
+            break;
+        } else {
+            break;
+        }
+    }
+    return L;
+}
+
+// ============================================================================ the kernel
+__device__ __forceinline__ uint32_t morton_decode_1(uint32_t a)
+{
+    a = a & 0x55555555u;
+    a = (a | (a >> 1)) & 0x33333333u;
+    a = (a | (a >> 2)) & 0x0F0F0F0Fu;
+    a = (a | (a >> 4)) & 0x00FF00FFu;
+    a = (a | (a >> 8)) & 0x0000FFFFu;
+    return a;
+}
+
+constexpr int WAVES_PER_BLOCK = 4;
+
+// Persistent kernel: 4 waves per block share the LDS RSQRTSS table; each wave independently
+// pulls 8x8 tiles from the queue (TileScheduler::get_next_tile) and owns one MT state slot.
+extern "C" __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) sp_render_kernel(Scene sc, RenderArgs args)
+{
+    extern __shared__ uint32_t lds[];
+    const int tid  = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int rs_words = 2 << sc.rsqrt_bits;
+    for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
+    __syncthreads();
+    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+    Stack st{ lds + rs_words + wave * sc.stack_depth * 64, lane };
+
+    const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;
+    Rng          rng;
+    rng.base = args.mt_state + gwave * (2 * MT_N * 64) + lane;
+
+    uint32_t rays_total = 0, shadow_total = 0, samples_total = 0, draws_total = 0;
+    const uint32_t dx = morton_decode_1((uint32_t)lane);
+    const uint32_t dy = morton_decode_1((uint32_t)lane >> 1);
+    while (true) {
+        int grabbed = 0;
+        if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
+        const int64_t slot = __shfl(grabbed, 0, 64);
+        if (slot >= args.num_tiles) break;
+        const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
+        const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
+        const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
+        const bool     inside = (int)px < sc.width && (int)py < sc.height;
+        rgb            acc    = mkc(0, 0, 0);
+        if (inside) {
+            const uint32_t pix_seed = (px << 16u) | py;
+            rng_seed(rng, pix_seed ^ 0xb0ae9d99u);          // get_integrator_sampler (main.cpp:73)
+            const uint32_t seed2d = pix_seed ^ 0x6184faf4u; // RSequenceSampler m_seed_2D (main.cpp:67)
+            Ctx c{ sc, rng, q, st, 0u, 0u };
+            for (uint32_t i = 0; i < args.spp; ++i) {
+                rng_prepare(rng);
+                // RSequenceSampler::get_next_2D (math/Sampler.h:158) with count i
+                const float sx = rseq_component(seed2d, sc.alpha2_0, i);
+                const float sy = rseq_component(seed2d, sc.alpha2_1, i);
+                const float fx = (float)(int)px + sx;
+                const float fy = (float)(int)py + sy;
+                // PerspectiveCamera::generate_ray_impl (Cameras/Camera.h:119)
+                Ray ray;
+                ray.o = sc.camera.p;
+                ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
+                rgb L;
+                switch (args.integrator) {
+                case SP_INTEGRATOR_BRUTE_FORCE: L = integrate_bruteforce(c, ray); break;
+                case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE: L = integrate_iterative<false>(c, ray); break;
+                case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: L = integrate_iterative<true>(c, ray); break;
+                case SP_INTEGRATOR_ITERATIVE_RRNEE: L = integrate_rrnee(c, ray); break;
+                case SP_INTEGRATOR_WHITTED: L = integrate_whitted(c, ray); break;
+                default: L = integrate_direct(c, ray); break;
+                }
+                acc = cadd(acc, L); // image(p) += integrate(...)
+            }
+            acc = cdivs(acc, (float)args.spp); // image(p) /= num_pixel_samples
+            rays_total += c.rays;
+            shadow_total += c.shadow;
+            samples_total += args.spp;
+            draws_total += rng.draws;
+        }
+        float* o = args.out + ((size_t)slot * 64 + lane) * 3;
+        o[0]     = acc.r;
+        o[1]     = acc.g;
+        o[2]     = acc.b;
+    }
+    unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
+    for (int k = 0; k < 4; ++k) {
+        unsigned long long s = v[k];
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+        if (lane == 0 && s) atomicAdd(args.counters + k, s);
+    }
+}
+
+} // namespace spd
+
+// ============================================================================ host launch helpers
+namespace spd {
+hipError_t launch_render(const Scene& sc, const RenderArgs& args, int blocks, size_t lds_bytes, hipStream_t stream)
+{
+    hipLaunchKernelGGL(sp_render_kernel, dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);
+    return hipGetLastError();
+}
+
+int render_blocks_per_cu(size_t lds_bytes)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sp_render_kernel, 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess)
+        return 1;
+    return n > 0 ? n : 1;
+}
+} // namespace spd

@@ -1,0 +1,236 @@
+// sp_bvh.cpp -- bounding volume hierarchies over the bounded primitives.
+//
+// build_bvh_reference restates shapes/BVHAccelerator.h:173 `construct` exactly (same split
+// axis, same split position, libstdc++ std::partition element order, same leaf contents and
+// order) so a depth-first, child-0-first traversal visits primitives in the reference's order
+// and resolves equal-distance ties identically.  build_bvh_sah is the throughput build: binned
+// SAH (Wald 2007) with the same node format; it changes only the visiting order.
+#include "sp_host.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+
+namespace sph {
+
+namespace {
+struct Box {
+    float lo[3], hi[3];
+};
+Box empty_box()
+{
+    Box b;
+    for (int i = 0; i < 3; ++i) {
+        b.lo[i] = INFINITY;
+        b.hi[i] = -INFINITY;
+    }
+    return b;
+}
+// merge (math/BBox.h:192) with _mm_min_ps / _mm_max_ps operand order
+Box merge(const Box& a, const PrimBounds& b)
+{
+    Box r;
+    for (int i = 0; i < 3; ++i) {
+        r.lo[i] = spm::sse_min(a.lo[i], b.lo[i]);
+        r.hi[i] = spm::sse_max(a.hi[i], b.hi[i]);
+    }
+    return r;
+}
+float center_of(const PrimBounds& b, int d) { return (b.lo[d] + b.hi[d]) / 2.0f; }
+
+struct RefBuilder {
+    const std::vector<PrimBounds>& bounds;
+    std::vector<int32_t>           ids;
+    std::vector<BvhNode>           nodes;
+    int                            max_depth = 0;
+
+    uint32_t build(size_t first, size_t last, int depth)
+    {
+        max_depth = std::max(max_depth, depth);
+        Box bb    = empty_box();
+        for (size_t i = first; i < last; ++i) bb = merge(bb, bounds[ids[i]]);
+        const uint32_t me = static_cast<uint32_t>(nodes.size());
+        nodes.push_back(BvhNode{});
+        auto make_leaf = [&]() {
+            BvhNode& n = nodes[me];
+            for (int i = 0; i < 3; ++i) { n.lo[i] = bb.lo[i]; n.hi[i] = bb.hi[i]; }
+            n.a = static_cast<uint32_t>(first);
+            n.b = static_cast<uint32_t>(last - first) | BVH_LEAF;
+            return me;
+        };
+        if (last - first <= 4) return make_leaf();
+        // max_dim(bounds.size()) (math/Vector3.h:654)
+        const float sx = std::fabs(bb.hi[0] - bb.lo[0]);
+        const float sy = std::fabs(bb.hi[1] - bb.lo[1]);
+        const float sz = std::fabs(bb.hi[2] - bb.lo[2]);
+        int         dim;
+        if (sx > sy) dim = (sx > sz) ? 0 : 2;
+        else dim = (sy > sz) ? 1 : 2;
+        const float split_point = (bb.lo[dim] + bb.hi[dim]) / 2.0f;
+        const size_t split = stl_partition(ids, first, last, [&](int32_t id) { return center_of(bounds[id], dim) < split_point; });
+        if (split == first || split == last) return make_leaf();
+        const uint32_t l = build(first, split, depth + 1);
+        const uint32_t r = build(split, last, depth + 1);
+        BvhNode& n = nodes[me];
+        for (int i = 0; i < 3; ++i) { n.lo[i] = bb.lo[i]; n.hi[i] = bb.hi[i]; }
+        n.a = l;
+        n.b = r;
+        return me;
+    }
+};
+} // namespace
+
+Bvh build_bvh_reference(const std::vector<PrimBounds>& bounds)
+{
+    Bvh        out;
+    RefBuilder b{ bounds, {}, {} };
+    b.ids.resize(bounds.size());
+    for (size_t i = 0; i < bounds.size(); ++i) b.ids[i] = static_cast<int32_t>(i);
+    if (!bounds.empty()) b.build(0, bounds.size(), 1);
+    out.nodes      = std::move(b.nodes);
+    out.prim_order = std::move(b.ids);
+    out.max_depth  = b.max_depth;
+    return out;
+}
+
+// ------------------------------------------------------------------------------ binned SAH
+namespace {
+struct SahBuilder {
+    const std::vector<PrimBounds>& bounds;
+    std::vector<int32_t>           ids;
+    std::vector<float>             cx, cy, cz;
+    std::vector<BvhNode>           nodes;
+    int                            max_leaf;
+    int                            max_depth = 0;
+
+    static float area(const Box& b)
+    {
+        const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+        if (!(dx >= 0.0f)) return 0.0f;
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+    const float* cen(int d) const { return d == 0 ? cx.data() : (d == 1 ? cy.data() : cz.data()); }
+
+    uint32_t build(size_t first, size_t last, int depth)
+    {
+        max_depth = std::max(max_depth, depth);
+        Box bb = empty_box(), cb = empty_box();
+        for (size_t i = first; i < last; ++i) {
+            const int32_t id = ids[i];
+            bb               = merge(bb, bounds[id]);
+            PrimBounds c;
+            c.lo[0] = c.hi[0] = cx[id];
+            c.lo[1] = c.hi[1] = cy[id];
+            c.lo[2] = c.hi[2] = cz[id];
+            cb = merge(cb, c);
+        }
+        const uint32_t me = static_cast<uint32_t>(nodes.size());
+        nodes.push_back(BvhNode{});
+        const size_t n = last - first;
+        auto make_leaf = [&]() {
+            BvhNode& nd = nodes[me];
+            for (int i = 0; i < 3; ++i) { nd.lo[i] = bb.lo[i]; nd.hi[i] = bb.hi[i]; }
+            nd.a = static_cast<uint32_t>(first);
+            nd.b = static_cast<uint32_t>(n) | BVH_LEAF;
+            return me;
+        };
+        if (n <= 1) return make_leaf();
+        constexpr int BINS = 32;
+        float best_cost = INFINITY;
+        int   best_dim = -1, best_bin = -1;
+        for (int d = 0; d < 3; ++d) {
+            const float lo = cb.lo[d], hi = cb.hi[d];
+            if (!(hi > lo)) continue;
+            const float  k = BINS * (1.0f - 1e-5f) / (hi - lo);
+            Box          bins[BINS];
+            int          cnt[BINS] = {};
+            for (auto& b : bins) b = empty_box();
+            const float* c = cen(d);
+            for (size_t i = first; i < last; ++i) {
+                const int32_t id = ids[i];
+                int           bi = static_cast<int>((c[id] - lo) * k);
+                bi               = std::min(std::max(bi, 0), BINS - 1);
+                cnt[bi]++;
+                bins[bi] = merge(bins[bi], bounds[id]);
+            }
+            float right_area[BINS];
+            int   right_cnt[BINS];
+            Box   acc = empty_box();
+            int   ac  = 0;
+            for (int b = BINS - 1; b > 0; --b) {
+                PrimBounds pb;
+                for (int i = 0; i < 3; ++i) { pb.lo[i] = bins[b].lo[i]; pb.hi[i] = bins[b].hi[i]; }
+                if (cnt[b]) acc = merge(acc, pb);
+                ac += cnt[b];
+                right_area[b] = area(acc);
+                right_cnt[b]  = ac;
+            }
+            acc = empty_box();
+            ac  = 0;
+            for (int b = 0; b < BINS - 1; ++b) {
+                PrimBounds pb;
+                for (int i = 0; i < 3; ++i) { pb.lo[i] = bins[b].lo[i]; pb.hi[i] = bins[b].hi[i]; }
+                if (cnt[b]) acc = merge(acc, pb);
+                ac += cnt[b];
+                if (ac == 0 || right_cnt[b + 1] == 0) continue;
+                const float cost = area(acc) * ac + right_area[b + 1] * right_cnt[b + 1];
+                if (cost < best_cost) { best_cost = cost; best_dim = d; best_bin = b; }
+            }
+        }
+        const float leaf_cost = area(bb) * static_cast<float>(n);
+        // traversal cost ~ 1 triangle test per node visit; stop when the split does not pay
+        if (best_dim < 0 || (n <= static_cast<size_t>(max_leaf) && best_cost + area(bb) >= leaf_cost)) {
+            if (best_dim < 0 && n > static_cast<size_t>(max_leaf)) {
+                // all centroids coincide: median split by index
+                const size_t mid = first + n / 2;
+                const uint32_t l = build(first, mid, depth + 1);
+                const uint32_t r = build(mid, last, depth + 1);
+                BvhNode& nd = nodes[me];
+                for (int i = 0; i < 3; ++i) { nd.lo[i] = bb.lo[i]; nd.hi[i] = bb.hi[i]; }
+                nd.a = l; nd.b = r;
+                return me;
+            }
+            return make_leaf();
+        }
+        const float  lo = cb.lo[best_dim], hi = cb.hi[best_dim];
+        const float  k  = BINS * (1.0f - 1e-5f) / (hi - lo);
+        const float* c  = cen(best_dim);
+        auto mid_it = std::stable_partition(ids.begin() + first, ids.begin() + last, [&](int32_t id) {
+            int bi = static_cast<int>((c[id] - lo) * k);
+            bi     = std::min(std::max(bi, 0), BINS - 1);
+            return bi <= best_bin;
+        });
+        size_t mid = static_cast<size_t>(mid_it - ids.begin());
+        if (mid == first || mid == last) mid = first + n / 2;
+        const uint32_t l = build(first, mid, depth + 1);
+        const uint32_t r = build(mid, last, depth + 1);
+        BvhNode& nd = nodes[me];
+        for (int i = 0; i < 3; ++i) { nd.lo[i] = bb.lo[i]; nd.hi[i] = bb.hi[i]; }
+        nd.a = l;
+        nd.b = r;
+        return me;
+    }
+};
+} // namespace
+
+Bvh build_bvh_sah(const std::vector<PrimBounds>& bounds, int max_leaf)
+{
+    Bvh        out;
+    SahBuilder b{ bounds, {}, {}, {}, {}, {}, max_leaf };
+    const size_t n = bounds.size();
+    b.ids.resize(n);
+    b.cx.resize(n); b.cy.resize(n); b.cz.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+        b.ids[i] = static_cast<int32_t>(i);
+        b.cx[i]  = center_of(bounds[i], 0);
+        b.cy[i]  = center_of(bounds[i], 1);
+        b.cz[i]  = center_of(bounds[i], 2);
+    }
+    if (n) b.build(0, n, 1);
+    out.nodes      = std::move(b.nodes);
+    out.prim_order = std::move(b.ids);
+    out.max_depth  = b.max_depth;
+    return out;
+}
+
+} // namespace sph

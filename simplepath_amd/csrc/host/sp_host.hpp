@@ -1,0 +1,156 @@
+// sp_host.hpp -- host-side scene model of the MI355X SimplePath renderer.
+//
+// Mirrors what the reference's FileParser (base/FileParser.cpp) and Scene (base/Scene.h) build,
+// flattened into arrays that can be copied to HBM.  All transforms, mesh vertices/normals,
+// material constants and camera vectors are computed on the host with the reference's own
+// arithmetic (sp_math.h helpers + the host CPU's RSQRTSS + glibc libm) so the device sees the
+// exact same bits the reference would hold in memory.
+#pragma once
+
+#include "../common/sp_math.h"
+#include "../../../include/simplepath_hip.h"
+
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace sph {
+
+using spm::aff;
+using spm::f3;
+using spm::lin;
+using spm::rgb;
+
+struct SpError : std::runtime_error {
+    int code;
+    SpError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// ---- host versions of the reference's vector ops that need RSQRTSS ----------------------------
+inline float host_rsqrt(float a) { return spm::rsqrt_newton(a, spm::rsqrtss_host(a)); }
+inline f3 host_normalize(f3 a) { return spm::scale(a, host_rsqrt(spm::dot(a, a))); }
+
+// Transformation<T> (math/Transformation.h:37): forward and inverse kept side by side.
+struct AffXf {
+    aff fwd, inv;
+};
+
+aff  aff_identity();
+lin  lin_identity();
+aff  aff_mul(const aff& a, const aff& b);  // AffineSpace * AffineSpace
+aff  aff_mul_lin(const aff& a, const lin& b);  // AffineSpace * LinearSpace3x3
+aff  lin_mul_aff(const lin& a, const aff& b);  // LinearSpace3x3 * AffineSpace
+lin  lin_mul(const lin& a, const lin& b);
+lin  lin_inverse(const lin& a);            // adjoint() / determinant()
+lin  lin_transposed(const lin& a);
+lin  normal_matrix(const aff& m);          // m.linear.inverse().transposed()
+f3   xfm_normal(const lin& nm, f3 n);      // madd chain with the normal matrix
+
+struct Material {
+    sp_material_desc d;
+};
+
+struct Mesh {
+    std::vector<f3>       vertices; // world space
+    std::vector<f3>       normals;  // transformed, not re-normalised
+    std::vector<uint32_t> indices;
+};
+
+struct Scene {
+    int         image_width  = 512; // FileParser defaults (base/FileParser.cpp:256-259)
+    int         image_height = 512;
+    int         rr_depth     = 3;
+    int         max_depth    = 10;
+    int         integrator   = SP_INTEGRATOR_NOT_SPECIFIED;
+    std::string output_file_name;
+    bool        has_camera = false;
+    // camera parameters kept so the resolution can be overridden
+    f3    cam_origin{}, cam_look_at{}, cam_up{};
+    float cam_fov_deg = 45.0f;
+    aff   camera{};
+
+    std::vector<Material>       materials;
+    std::vector<std::string>    material_names;
+    std::vector<sp_xform_shape> shapes;
+    std::vector<sp_light_desc>  lights;
+    // triangles of all meshes, concatenated (global vertex numbering)
+    std::vector<f3>       vertices;
+    std::vector<f3>       normals;
+    std::vector<uint32_t> indices;
+    std::vector<int32_t>  tri_material;
+    // Scene::m_geometry order
+    std::vector<int32_t> prim_kind;
+    std::vector<int32_t> prim_index;
+
+    void rebuild_camera();
+};
+
+std::unique_ptr<Scene> parse_scene(const std::string& text, const std::string& base_dir);
+std::unique_ptr<Scene> parse_scene_file(const std::string& path);
+
+// Camera (Cameras/Camera.h:99 PerspectiveCamera::create_transform)
+aff perspective_camera_transform(f3 eye, f3 look_at, f3 up, float fov_degrees, int w, int h);
+
+// RSequence<dim> alphas (math/Sampler.h:47), computed with glibc powf like the reference.
+void rsequence_alphas(float alpha1[1], float alpha2[2]);
+
+// ---- BVH ---------------------------------------------------------------------------------------
+// Binary BVH node, 32 bytes: bounds + (left child, right child) or (first prim, count | LEAF_BIT).
+struct BvhNode {
+    float    lo[3];
+    uint32_t a;   // internal: left child index;  leaf: first primitive slot
+    float    hi[3];
+    uint32_t b;   // internal: right child index; leaf: count | 0x80000000
+};
+static_assert(sizeof(BvhNode) == 32, "BvhNode layout");
+constexpr uint32_t BVH_LEAF = 0x80000000u;
+
+struct Bvh {
+    std::vector<BvhNode> nodes;
+    std::vector<int32_t> prim_order; // slot -> primitive id (into the bounded list given)
+    int                  max_depth = 0;
+};
+
+struct PrimBounds {
+    float lo[3], hi[3];
+};
+
+// Reference construction (shapes/BVHAccelerator.h:173): midpoint split on the longest axis with
+// libstdc++'s std::partition (unstable, two-sided swap), leaves of <= 4, leaf on failed split.
+Bvh build_bvh_reference(const std::vector<PrimBounds>& bounds);
+// Binned SAH construction (product default).
+Bvh build_bvh_sah(const std::vector<PrimBounds>& bounds, int max_leaf = 4);
+
+// libstdc++ std::partition on a bidirectional range, returning the split point.
+template <typename T, typename Pred>
+size_t stl_partition(std::vector<T>& v, size_t first, size_t last, Pred pred)
+{
+    while (true) {
+        while (true) {
+            if (first == last) return first;
+            if (pred(v[first])) ++first;
+            else break;
+        }
+        --last;
+        while (true) {
+            if (first == last) return first;
+            if (!pred(v[last])) --last;
+            else break;
+        }
+        std::swap(v[first], v[last]);
+        ++first;
+    }
+}
+
+// RSQRTSS table capture (sp_rsqrt.cpp)
+struct RsqrtCapture {
+    std::vector<uint32_t> entries;
+    int32_t               bits     = 0;
+    bool                  verified = false;
+    uint32_t              zero_result = 0, denorm_result = 0;
+};
+const RsqrtCapture& rsqrt_capture();
+
+} // namespace sph

@@ -1,0 +1,259 @@
+"""Benchmark / test workloads: the reference's scene descriptions and synthetic meshes.
+
+The reference's scenes (scenes/bunny.sp, example_scene.sp, scenes/material_spheres.sp ...) name
+PLY/STL/PFM assets that are not part of the repository (Stanford bunny `bun_zipper.ply`, lucy,
+an HDR environment map).  There is no network here, so the meshes are generated: a closed,
+smooth, star-shaped "bunny-like" surface with the same vertex/face counts class (~35k vertices,
+~69.5k triangles) and the same bounding box as bun_zipper.ply, written in the same PLY layout
+(binary_little_endian, float x y z confidence intensity, `list uchar int vertex_indices`).  The
+scene parameters (camera, materials, transforms, lights) are those of the reference files.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+# bounding box of the Stanford bunny reconstruction bun_zipper.ply
+_BUNNY_LO = np.array([-0.0946899, 0.0329874, -0.0618736])
+_BUNNY_HI = np.array([0.0610398, 0.187321, 0.0587997])
+
+
+def _bunny_radius(d: np.ndarray) -> np.ndarray:
+    """Radial profile r(direction) of the synthetic bunny: an ellipsoidal body with head, ears and tail lobes."""
+    lobes = [  # centre direction, width, amplitude
+        ((0.55, 0.35, 0.0), 0.35, 0.55),    # head (forward, up)
+        ((0.35, 0.85, 0.18), 0.05, 0.95),   # ear 1
+        ((0.30, 0.88, -0.22), 0.05, 0.90),  # ear 2
+        ((-0.95, 0.1, 0.0), 0.08, 0.25),    # tail
+        ((0.2, -0.9, 0.0), 0.4, -0.15),     # flattened belly
+    ]
+    r = np.full(d.shape[0], 1.0)
+    for c, w, a in lobes:
+        c = np.asarray(c, dtype=np.float64)
+        c = c / np.linalg.norm(c)
+        dist2 = np.sum((d - c) ** 2, axis=1)
+        r += a * np.exp(-dist2 / w)
+    # gentle high-frequency ripples so the surface is not a smooth ellipsoid
+    r += 0.015 * np.sin(23.0 * d[:, 0]) * np.cos(19.0 * d[:, 1]) * np.sin(17.0 * d[:, 2])
+    return r
+
+
+def bunny_mesh(n_lat: int = 185, n_lon: int = 188):
+    """Closed lat-long surface: n_lat*n_lon + 2 vertices, 2*n_lon*n_lat triangles (CCW, outward)."""
+    theta = np.pi * (np.arange(1, n_lat + 1) / (n_lat + 1))  # exclude poles
+    phi = 2.0 * np.pi * (np.arange(n_lon) / n_lon)
+    th, ph = np.meshgrid(theta, phi, indexing="ij")
+    d = np.stack([np.sin(th) * np.cos(ph), np.cos(th), np.sin(th) * np.sin(ph)], axis=-1).reshape(-1, 3)
+    poles = np.array([[0.0, 1.0, 0.0], [0.0, -1.0, 0.0]])
+    d = np.concatenate([d, poles], axis=0)
+    p = d * _bunny_radius(d)[:, None] * np.array([1.25, 1.0, 0.8])
+    lo, hi = p.min(axis=0), p.max(axis=0)
+    p = _BUNNY_LO + (p - lo) / (hi - lo) * (_BUNNY_HI - _BUNNY_LO)
+    verts = p.astype(np.float32)
+    top, bot = n_lat * n_lon, n_lat * n_lon + 1
+
+    def vid(i, j):
+        return i * n_lon + (j % n_lon)
+
+    faces = []
+    j = np.arange(n_lon)
+    for i in range(n_lat - 1):
+        a, b, c, e = vid(i, j), vid(i, j + 1), vid(i + 1, j), vid(i + 1, j + 1)
+        faces.append(np.stack([a, b, c], 1))
+        faces.append(np.stack([b, e, c], 1))
+    faces.append(np.stack([np.full(n_lon, top), vid(0, j + 1), vid(0, j)], 1))
+    faces.append(np.stack([np.full(n_lon, bot), vid(n_lat - 1, j), vid(n_lat - 1, j + 1)], 1))
+    f = np.concatenate(faces).astype(np.int32)
+    # orient outward: flip if the first face's normal points to the centre
+    v0, v1, v2 = verts[f[:, 0]], verts[f[:, 1]], verts[f[:, 2]]
+    n = np.cross(v1 - v0, v2 - v0)
+    ctr = verts.mean(axis=0)
+    if np.sum(np.einsum("ij,ij->i", n, (v0 + v1 + v2) / 3 - ctr) < 0) > f.shape[0] // 2:
+        f = f[:, [0, 2, 1]]
+    return verts, f
+
+
+def write_ply(path: str, verts: np.ndarray, faces: np.ndarray) -> None:
+    """binary_little_endian PLY in the layout of bun_zipper.ply."""
+    nv, nf = verts.shape[0], faces.shape[0]
+    header = ("ply\nformat binary_little_endian 1.0\ncomment synthetic stand-in for bun_zipper.ply\n"
+              f"element vertex {nv}\nproperty float x\nproperty float y\nproperty float z\n"
+              "property float confidence\nproperty float intensity\n"
+              f"element face {nf}\nproperty list uchar int vertex_indices\nend_header\n").encode()
+    vrec = np.zeros(nv, dtype=[("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("c", "<f4"), ("i", "<f4")])
+    vrec["x"], vrec["y"], vrec["z"] = verts[:, 0], verts[:, 1], verts[:, 2]
+    vrec["c"], vrec["i"] = 1.0, 0.5
+    frec = np.zeros(nf, dtype=[("n", "u1"), ("a", "<i4"), ("b", "<i4"), ("c", "<i4")])
+    frec["n"] = 3
+    frec["a"], frec["b"], frec["c"] = faces[:, 0], faces[:, 1], faces[:, 2]
+    with open(path, "wb") as fh:
+        fh.write(header)
+        fh.write(vrec.tobytes())
+        fh.write(frec.tobytes())
+
+
+def ensure_bunny_ply(directory: str) -> str:
+    rel = os.path.join("ply_files", "bunny", "reconstruction", "bun_zipper.ply")
+    path = os.path.join(directory, rel)
+    if not os.path.exists(path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        v, f = bunny_mesh()
+        tmp = path + ".tmp%d" % os.getpid()
+        write_ply(tmp, v, f)
+        os.replace(tmp, path)
+    return rel
+
+
+# scenes/bunny.sp of the reference: four bunnies (two clearcoat, lambertian, glossy), a glossy
+# plane and a sphere light; 1000x600 as written (the benchmark overrides the resolution).
+def bunny_sp(ply_rel: str) -> str:
+    mats = [
+        ("material_lambertian", "material_lambertian", {"diffuse": "0.1 0.8 0.8"}),
+        ("material_lambertian", "material_lambertian_base", {"diffuse": "0.1 0.2 0.8"}),
+        ("material_glossy", "material_glossy_base", {"diffuse": "0.8 0.2 0.8", "ior": "1.8", "roughness": "0.25"}),
+        ("material_glossy", "material_glossy", {"diffuse": "0.8 0.2 0.2", "ior": "1.8", "roughness": "0.75"}),
+        ("material_glossy", "material_glossy_plane", {"diffuse": "0.6 0.6 0.6", "ior": "1.8", "roughness": "0.01"}),
+        ("material_clearcoat", "material_lambertian_clearcoat",
+         {"base": '"material_lambertian_base"', "ior": "1.5", "color": "1.0 0.8 0.8"}),
+        ("material_clearcoat", "material_glossy_clearcoat",
+         {"base": '"material_glossy_base"', "ior": "1.3", "color": "1.0 1.0 1.0"}),
+    ]
+    out = ["version: 1", "", "scene_parameters {", '    output_file_name: "image.pfm"',
+           "    width: 1000", "    height: 600", "}", "",
+           "perspective_camera {", "    origin: 0.0 2.0 5.0", "    look_at: -0.25 1.0 0.0", "    fov: 45", "}", ""]
+    for kind, name, attrs in mats:
+        out.append(kind + " {")
+        out.append(f'    name: "{name}"')
+        for k, v in attrs.items():
+            out.append(f"    {k}: {v}")
+        out += ["}", ""]
+    for tx, mat in [(2.25, "material_glossy_clearcoat"), (0.75, "material_lambertian_clearcoat"),
+                    (-0.75, "material_lambertian"), (-2.25, "material_glossy")]:
+        out += ["mesh {", f'    file: "{ply_rel}"', f"    translate: {tx} 0.0 0.0",
+                "    scale: 10.0 10.0 10.0", f'    material: "{mat}"', "}", ""]
+    out += ["plane {", '    material: "material_glossy_plane"', "    translate: 0.0 0.329874 0.0", "}", "",
+            "sphere_light {", "    translate: 0.0 3.0 0.0", "    scale: 0.5 0.5 0.5",
+            "    radiance: 10.0 10.0 10.0", "}", ""]
+    return "\n".join(out)
+
+
+def write_bunny_scene(directory: str) -> str:
+    os.makedirs(directory, exist_ok=True)
+    rel = ensure_bunny_ply(directory)
+    path = os.path.join(directory, "bunny.sp")
+    with open(path, "w") as fh:
+        fh.write(bunny_sp(rel))
+    return path
+
+
+# scenes/material_spheres.sp with its image environment light replaced by a uniform
+# environment_light (the HDR map is not available; image lights are a later row).
+def spheres_sp(env_radiance: str = "1.0 1.0 1.0", with_sphere_light: bool = True) -> str:
+    s = """version: 1
+
+scene_parameters {
+    output_file_name: "spheres.pfm"
+    width: 450
+    height: 1500
+}
+
+perspective_camera {
+    origin: 0.0 0.0 10.0
+    look_at: 0.0 0.0 0.0
+    fov: 45
+}
+
+material_lambertian {
+    name: "material_lambertian"
+    diffuse: 0.1 0.8 0.8
+}
+
+material_lambertian {
+    name: "material_lambertian_base"
+    diffuse: 0.1 0.2 0.8
+}
+
+material_glossy {
+    name: "material_glossy_base"
+    diffuse: 0.8 0.2 0.8
+    ior: 1.8
+    roughness: 0.25
+}
+
+material_glossy {
+    name: "material_glossy"
+    diffuse: 0.8 0.2 0.2
+    ior: 1.8
+    roughness: 0.75
+}
+
+material_glossy {
+    name: "material_glossy_plane"
+    diffuse: 0.6 0.6 0.6
+    ior: 1.8
+    roughness: 0.01
+}
+
+material_clearcoat {
+    name: "material_lambertian_clearcoat"
+    base: "material_lambertian_base"
+    ior: 1.5
+    color: 1.0 0.8 0.8
+}
+
+material_clearcoat {
+    name: "material_glossy_clearcoat"
+    base: "material_glossy_base"
+    ior: 1.3
+    color: 1.0 1.0 1.0
+}
+
+sphere {
+    translate: 0.0 3.0 0.0
+    material: "material_glossy_clearcoat"
+}
+
+sphere {
+    translate: 0.0 1.0 0.0
+    material: "material_lambertian_clearcoat"
+}
+
+sphere {
+    translate: 0.0 -1.0 0.0
+    material: "material_lambertian"
+}
+
+sphere {
+    translate: 0.0 -3.0 0.0
+    material: "material_glossy"
+}
+
+plane {
+    material: "material_glossy_plane"
+    rotate: 1 0 0 90
+    translate: 0.0 0.0 -1.0
+}
+
+environment_light {
+    rotate: 0.0 1.0 0.0 45.0
+    radiance: %s
+}
+""" % env_radiance
+    if with_sphere_light:
+        s += """
+sphere_light {
+    translate: 3.0 4.0 6.0
+    scale: 0.5 0.5 0.5
+    radiance: 20.0 20.0 20.0
+}
+"""
+    return s
+
+
+def write_spheres_scene(directory: str, with_sphere_light: bool = True) -> str:
+    os.makedirs(directory, exist_ok=True)
+    path = os.path.join(directory, "material_spheres.sp")
+    with open(path, "w") as fh:
+        fh.write(spheres_sp(with_sphere_light=with_sphere_light))
+    return path

@@ -1,0 +1,21 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the C-ABI on the device)")
+
+
+@pytest.fixture(scope="session")
+def scene_dir(tmp_path_factory):
+    from simplepath_amd import scenes
+    d = str(tmp_path_factory.mktemp("scenes"))
+    scenes.write_bunny_scene(d)
+    scenes.write_spheres_scene(d)
+    return d

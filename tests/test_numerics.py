@@ -1,0 +1,37 @@
+"""Numerics contract: samplers and RSQRTSS emulation against their golden sources."""
+import ctypes as C
+import os
+
+import numpy as np
+
+import simplepath_amd as sp
+from tests import _oracle
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sampler_golden.npy")
+
+
+def test_oracle_sampler_matches_libstdcxx_golden():
+    g = np.load(GOLD)
+    L = _oracle.load("glibc")
+    for (x, y) in {(int(a), int(b)) for a, b, _ in g}:
+        rows = g[(g[:, 0] == x) & (g[:, 1] == y)][:, 2]
+        out = np.zeros(rows.size, dtype=np.float32)
+        L.orc_mt_stream(((x << 16) | y) ^ 0xB0AE9D99, rows.size, out.ctypes.data_as(C.POINTER(C.c_float)))
+        assert np.array_equal(out.view(np.uint32), rows), (x, y)
+
+
+def test_rsqrt_table_verified_against_host_instruction():
+    bits, ok = C.c_int32(), C.c_int32()
+    sp.lib().sp_rsqrt_table_info(C.byref(bits), C.byref(ok))
+    assert ok.value == 1 and 8 <= bits.value <= 23
+    L = _oracle.load("glibc")
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(1e-6, 1e6, 20000).astype(np.float32),
+                         np.array([1.0, 2.0, 4.0, 0.25, 3.0e-38, 1.0e38], dtype=np.float32)])
+    for x in xs:
+        # the emulated RSQRTSS then the reference's Newton step == oracle's intrinsic path
+        r = sp.lib().sp_host_rsqrt_emulated(float(x))
+        r32 = np.float32(r)
+        a = np.float32(x)
+        newton = np.float32(np.float32(1.5) * r32) + np.float32(np.float32(np.float32(a * np.float32(-0.5)) * r32) * np.float32(r32 * r32))
+        assert np.float32(L.orc_rsqrt(float(x))) == newton

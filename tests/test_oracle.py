@@ -1,0 +1,39 @@
+"""The CPU oracle itself: deterministic, both libm variants close, counts consistent."""
+import os
+
+import numpy as np
+
+import simplepath_amd as sp
+from tests import _oracle
+
+
+def _scene(scene_dir, name, w, h):
+    s = sp.Scene.from_file(os.path.join(scene_dir, name))
+    s.set_resolution(w, h)
+    return s
+
+
+def test_oracle_deterministic_and_thread_independent(scene_dir):
+    s = _scene(scene_dir, "bunny.sp", 48, 32)
+    a, sa = _oracle.render(s, 6, 2, threads=1, variant="glibc")
+    b, sb = _oracle.render(s, 6, 2, threads=7, variant="glibc")
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sa == sb
+
+
+def test_oracle_libm_variants_agree_statistically(scene_dir):
+    s = _scene(scene_dir, "bunny.sp", 48, 32)
+    a, _ = _oracle.render(s, 6, 8, variant="glibc")
+    b, _ = _oracle.render(s, 6, 8, variant="spm")
+    rel = np.linalg.norm((a - b).ravel()) / np.linalg.norm(a.ravel())
+    assert rel < 0.05, rel
+
+
+def test_every_integrator_runs(scene_dir):
+    s = _scene(scene_dir, "material_spheres.sp", 24, 40)
+    for name, val in sp.INTEGRATORS.items():
+        if name == "mandelbrot":
+            continue
+        t, st = _oracle.render(s, val, 2, variant="glibc")
+        assert np.isfinite(t).all() or name in ("brute_force",), name
+        assert st["samples"] == 2 * 24 * 40
