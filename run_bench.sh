@@ -6,6 +6,6 @@ export TMPDIR=/tmp
 timeout -k 10 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 10 > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench exit $rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
 [ $rc -eq 0 ] || exit $rc
-cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof.err
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof.err
 echo "rocprof exit $?"
 find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*stats*" | head
