@@ -4,13 +4,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 namespace spd {
-hipError_t launch_render(const Scene& sc, const RenderArgs& args, int blocks, size_t lds_bytes, hipStream_t stream);
-int        render_blocks_per_cu(size_t lds_bytes);
+hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
+                         hipStream_t stream);
+int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
 } // namespace spd
 
 namespace {
@@ -508,7 +510,9 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
     hipDeviceProp_t prop;
     SP_HIP(hipGetDeviceProperties(&prop, s->device));
-    const int     per_cu  = spd::render_blocks_per_cu(lds_bytes);
+    int variant = 0;
+    if (const char* v = std::getenv("SP_KERNEL_VARIANT")) variant = std::atoi(v);
+    const int     per_cu  = spd::render_blocks_per_cu(integ, variant, lds_bytes);
     const int64_t max_blk = (int64_t)prop.multiProcessorCount * per_cu;
     const int64_t need    = (n_tiles + 3) / 4;
     const int     blocks  = (int)std::max<int64_t>(1, std::min(max_blk, need));
@@ -532,7 +536,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     a.mt_state     = s->mt_state;
     a.counters     = s->counters;
     SP_HIP(hipEventRecord(s->ev0, stream));
-    SP_HIP(spd::launch_render(s->dev, a, blocks, lds_bytes, stream));
+    SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
     SP_HIP(hipEventRecord(s->ev1, stream));
     SP_HIP(hipEventSynchronize(s->ev1));
     if (stats) {
@@ -545,6 +549,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         stats->samples     = c[2];
         stats->rng_draws   = c[3];
         stats->kernel_ms   = ms;
+        stats->twist_ms    = (float)blocks; // diagnostic: persistent blocks launched
     }
     return SP_OK;
 }

@@ -43,7 +43,7 @@ struct Rng {
 __device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_N * 64; }
 
 // B = twist(A) without modifying A (in-place MT19937-64 twist split over two buffers).
-__device__ __noinline__ void mt_twist_into(const uint64_t* A, uint64_t* B)
+__device__ __forceinline__ void mt_twist_into(const uint64_t* A, uint64_t* B)
 {
     uint64_t ak = A[0];
 #pragma unroll 4
@@ -76,12 +76,20 @@ __device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
     r.draws = 0;
 }
 
-// Twist ahead at a wave-synchronous point (sample / bounce start) so lanes twist together.
+// Twist ahead at a wave-synchronous point (sample / bounce start).  A lane may compute its next
+// generation any time after starting the current one, so all lanes whose next buffer is stale
+// twist together -- but only once some lane is within RNG_MARGIN draws of exhausting its buffer.
+// Twists are thus batched (about one per 312 draws per wave instead of one per sample), and the
+// in-draw fallback (rng_raw) keeps the stream exact when a path draws more than the margin.
+constexpr int RNG_MARGIN = 96;
 __device__ __forceinline__ void rng_prepare(Rng& r)
 {
-    if (!r.ready && r.idx >= 96) {
-        mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
-        r.ready = 1;
+    const bool urgent = !r.ready && r.idx >= MT_N - RNG_MARGIN;
+    if (__any(urgent)) {
+        if (!r.ready) {
+            mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
+            r.ready = 1;
+        }
     }
 }
 
@@ -300,7 +308,7 @@ struct Stack {
 };
 
 // Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
-__device__ __noinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+__device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     Hit h;
     h.t    = tmax;
@@ -340,7 +348,7 @@ __device__ __noinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, flo
 }
 
 // any-hit over the geometry accelerator (ListAccelerator::intersect_p_impl)
-__device__ __noinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+__device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     for (int i = 0; i < sc.n_unbounded; ++i) {
         const Shape& s = sc.shapes[sc.unbounded[i]];
@@ -383,7 +391,7 @@ struct LightHit {
 };
 
 // Scene::intersect_lights (base/Scene.h:69): ListAccelerator{environment..., BVH(sphere lights)}
-__device__ __noinline__ LightHit scene_intersect_lights(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+__device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     LightHit lh;
     lh.hit = false;
@@ -432,7 +440,7 @@ __device__ __noinline__ LightHit scene_intersect_lights(const Scene& sc, const R
     return lh;
 }
 
-__device__ __noinline__ bool lights_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+__device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     if (sc.n_light_nodes == 0) return false; // environment lights never occlude
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
@@ -608,7 +616,7 @@ __device__ __forceinline__ float erfinv(float a)
 }
 
 // materials/Material.cpp:14 beckmann_sample11
-__device__ __noinline__ P2 beckmann_sample11(float cos_theta_i, float U1, float U2)
+__device__ __forceinline__ P2 beckmann_sample11(float cos_theta_i, float U1, float U2)
 {
     P2 s;
     if (cos_theta_i > .9999f) {
@@ -716,7 +724,7 @@ __device__ __forceinline__ float mf_pdf(const Material& m, f3 wo, f3 wi, const R
     const f3 wh = normalize(add(wo, wi), q);
     return beck_pdf(m, wo, wh) / (4.0f * dot(wo, wh));
 }
-__device__ __noinline__ MSample mf_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+__device__ __forceinline__ MSample mf_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
     MSample r;
     r.color = mkc(0, 0, 0);
@@ -737,7 +745,7 @@ __device__ __noinline__ MSample mf_sample(const Material& m, f3 wo, Rng& rng, co
     return r;
 }
 // BRDF::rho_impl default (materials/Material.h:299) for the microfacet lobe
-__device__ __noinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+__device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
     rgb r = mkc(0, 0, 0);
     for (unsigned i = 0; i < 16u; ++i) {
@@ -782,7 +790,7 @@ __device__ __forceinline__ MSample lambert_sample(const Material& m, Rng& rng)
 }
 
 // Local-space sample/eval/pdf of a non-clearcoat material (OneSampleMaterial).
-__device__ __noinline__ MSample onesample_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+__device__ __forceinline__ MSample onesample_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
     if (m.kind == SP_MAT_LAMBERTIAN) return lambert_sample(m, rng);
     float w[2];
@@ -833,7 +841,7 @@ __device__ __noinline__ MSample onesample_sample(const Material& m, f3 wo, Rng& 
     return out;
 }
 
-__device__ __noinline__ rgb onesample_eval(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
+__device__ __forceinline__ rgb onesample_eval(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
 {
     if (m.kind == SP_MAT_LAMBERTIAN) {
         const float w     = lambert_only_weight(m);
@@ -854,7 +862,7 @@ __device__ __noinline__ rgb onesample_eval(const Material& m, f3 wo, f3 wi, Rng&
     return r;
 }
 
-__device__ __noinline__ float onesample_pdf(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
+__device__ __forceinline__ float onesample_pdf(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
 {
     if (m.kind == SP_MAT_LAMBERTIAN) {
         const float w = lambert_only_weight(m);
@@ -950,7 +958,7 @@ __device__ __forceinline__ float sphere_pdf(const Light& l, f3 observer_world)
 }
 
 // Light::sample (Lights/Light.h:145) for SphereLight / EnvironmentLight
-__device__ __noinline__ LSample light_sample(const Light& l, f3 obs, f3 obs_n, P2 u, const Rsq& q)
+__device__ __forceinline__ LSample light_sample(const Light& l, f3 obs, f3 obs_n, P2 u, const Rsq& q)
 {
     LSample s;
     f3      wi;
@@ -1043,7 +1051,7 @@ __device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
     return L;
 }
 
-__device__ __noinline__ rgb integrate_direct(Ctx& c, Ray ray)
+__device__ __forceinline__ rgb integrate_direct(Ctx& c, Ray ray)
 {
     rgb L = mkc(0, 0, 0);
     if (0 >= c.sc.max_depth) return L;
@@ -1058,7 +1066,7 @@ __device__ __noinline__ rgb integrate_direct(Ctx& c, Ray ray)
 
 // BruteForceIntegratorIterative(RR) (Integrators/Integrator.cpp:160 / 211)
 template <bool RR>
-__device__ __noinline__ rgb integrate_iterative(Ctx& c, Ray ray)
+__device__ __forceinline__ rgb integrate_iterative(Ctx& c, Ray ray)
 {
     rgb   throughput = mkc(1, 1, 1);
     rgb   L          = mkc(0, 0, 0);
@@ -1100,7 +1108,7 @@ __device__ __noinline__ rgb integrate_iterative(Ctx& c, Ray ray)
 // BruteForceIntegrator (recursive, Integrators/Integrator.cpp:116), unrolled: the recursion's
 // product ((L_{k+1} * cos_k) * color_k) / pdf_k is folded back from the deepest level.
 constexpr int MAX_RECURSION = 32;
-__device__ __noinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
+__device__ __forceinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
 {
     float cosv[MAX_RECURSION];
     rgb   colv[MAX_RECURSION];
@@ -1137,7 +1145,7 @@ __device__ __noinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
 
 // WhittedIntegrator (Integrators/Integrator.cpp:323): NEE at every hit, recursion on specular.
 // L_k += do_integrate(child) folds right-nested: L_0 + (L_1 + (L_2 + ...)).
-__device__ __noinline__ rgb integrate_whitted(Ctx& c, Ray ray)
+__device__ __forceinline__ rgb integrate_whitted(Ctx& c, Ray ray)
 {
     rgb       Lv[MAX_RECURSION + 1];
     int       depth = 0;
@@ -1206,7 +1214,7 @@ __device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p,
 }
 
 // IntegratorIterativeRRNEE (Integrators/Integrator.cpp:550)
-__device__ __noinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
+__device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
 {
     rgb   throughput = mkc(1, 1, 1);
     rgb   L          = mkc(0, 0, 0);
@@ -1261,9 +1269,23 @@ __device__ __forceinline__ uint32_t morton_decode_1(uint32_t a)
 
 constexpr int WAVES_PER_BLOCK = 4;
 
+template <int INTEG>
+__device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
+{
+    if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE) return integrate_bruteforce(c, ray);
+    else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE) return integrate_iterative<false>(c, ray);
+    else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR) return integrate_iterative<true>(c, ray);
+    else if constexpr (INTEG == SP_INTEGRATOR_ITERATIVE_RRNEE) return integrate_rrnee(c, ray);
+    else if constexpr (INTEG == SP_INTEGRATOR_WHITTED) return integrate_whitted(c, ray);
+    else return integrate_direct(c, ray);
+}
+
 // Persistent kernel: 4 waves per block share the LDS RSQRTSS table; each wave independently
 // pulls 8x8 tiles from the queue (TileScheduler::get_next_tile) and owns one MT state slot.
-extern "C" __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) sp_render_kernel(Scene sc, RenderArgs args)
+// One instantiation per integrator so each carries only its own live state; MINW is the
+// __launch_bounds__ occupancy request (waves per SIMD) chosen by measurement.
+template <int INTEG, int MINW>
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(Scene sc, RenderArgs args)
 {
     extern __shared__ uint32_t lds[];
     const int tid  = threadIdx.x;
@@ -1308,16 +1330,7 @@ extern "C" __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) sp_render_ker
                 Ray ray;
                 ray.o = sc.camera.p;
                 ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
-                rgb L;
-                switch (args.integrator) {
-                case SP_INTEGRATOR_BRUTE_FORCE: L = integrate_bruteforce(c, ray); break;
-                case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE: L = integrate_iterative<false>(c, ray); break;
-                case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: L = integrate_iterative<true>(c, ray); break;
-                case SP_INTEGRATOR_ITERATIVE_RRNEE: L = integrate_rrnee(c, ray); break;
-                case SP_INTEGRATOR_WHITTED: L = integrate_whitted(c, ray); break;
-                default: L = integrate_direct(c, ray); break;
-                }
-                acc = cadd(acc, L); // image(p) += integrate(...)
+                acc   = cadd(acc, integrate<INTEG>(c, ray)); // image(p) += integrate(...)
             }
             acc = cdivs(acc, (float)args.spp); // image(p) /= num_pixel_samples
             rays_total += c.rays;
@@ -1342,16 +1355,48 @@ extern "C" __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) sp_render_ker
 
 // ============================================================================ host launch helpers
 namespace spd {
-hipError_t launch_render(const Scene& sc, const RenderArgs& args, int blocks, size_t lds_bytes, hipStream_t stream)
+using KernelFn = void (*)(Scene, RenderArgs);
+
+template <int MINW>
+KernelFn kernel_for(int integ)
 {
-    hipLaunchKernelGGL(sp_render_kernel, dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);
+    if constexpr (MINW != 2) {
+        if (integ == SP_INTEGRATOR_DIRECT_LIGHTING) return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, MINW>;
+        return kernel_for<2>(integ);
+    }
+    switch (integ) {
+    case SP_INTEGRATOR_BRUTE_FORCE: return sp_render_kernel<SP_INTEGRATOR_BRUTE_FORCE, MINW>;
+    case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE: return sp_render_kernel<SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE, MINW>;
+    case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: return sp_render_kernel<SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR, MINW>;
+    case SP_INTEGRATOR_ITERATIVE_RRNEE: return sp_render_kernel<SP_INTEGRATOR_ITERATIVE_RRNEE, MINW>;
+    case SP_INTEGRATOR_WHITTED: return sp_render_kernel<SP_INTEGRATOR_WHITTED, MINW>;
+    default: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, MINW>;
+    }
+}
+
+// variant = requested waves per SIMD for __launch_bounds__ (1..4); 0 = default choice
+KernelFn select_kernel(int integ, int variant)
+{
+    switch (variant) {
+    case 1: return kernel_for<1>(integ);
+    case 3: return kernel_for<3>(integ);
+    case 4: return kernel_for<4>(integ);
+    default: return kernel_for<2>(integ);
+    }
+}
+
+hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
+                         hipStream_t stream)
+{
+    hipLaunchKernelGGL(select_kernel(integ, variant), dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);
     return hipGetLastError();
 }
 
-int render_blocks_per_cu(size_t lds_bytes)
+int render_blocks_per_cu(int integ, int variant, size_t lds_bytes)
 {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sp_render_kernel, 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_kernel(integ, variant), 64 * WAVES_PER_BLOCK, lds_bytes) !=
+        hipSuccess)
         return 1;
     return n > 0 ? n : 1;
 }
