@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
     return ap.parse_args()
 
@@ -88,7 +89,8 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():
-        st = sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream)
+        st = sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
+                                    pipeline=args.pipeline, stage_timing=True)
         if dist is not None:
             dist.gather(out, gathered if rank == 0 else None, dst=0)
         return st
@@ -125,24 +127,7 @@ def main():
 
     mrays = rays / elapsed / 1e6
     msamples = samples / elapsed / 1e6
-    # ---- roofline of the dominant kernel (sp_render_kernel), per launch on this rank
-    per_launch_draws = sum(s.rng_draws for s in stats) / len(stats)
-    per_launch_pixels = min(len(my_tiles) * 64, args.width * args.height)
-    alg_bytes = per_launch_draws * MT_BYTES_PER_DRAW + per_launch_pixels * PIXEL_BYTES
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as fh:
-                tj = json.load(fh)
-            if tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "kernel": "sp_render_kernel", "kernel_ms": round(kernel_ms, 3),
-                "alg_bytes_per_launch": alg_bytes}
+    roofline = roofline_of(stats, min(len(my_tiles) * 64, args.width * args.height), args, kernel_ms)
 
     cpu = None
     parity = None
@@ -165,6 +150,7 @@ def main():
         "config": {"workload": f"bunny.sp {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
                    "width": args.width, "height": args.height, "spp": args.spp, "integrator": args.integrator,
                    "bvh": "sah" if args.bvh == 0 else "reference", "tiles": int(n_tiles),
+                   "pipeline": ["auto", "megakernel", "wavefront"][stats[-1].pipeline],
                    "parallelism": f"tiles{world}"},
         "msamples_per_s": round(msamples, 3),
         "rays_per_step": rays / args.steps,
@@ -175,6 +161,61 @@ def main():
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def stage_bytes(st, pixels):
+    """Algorithmic HBM bytes of each wavefront stage for one frame (DESIGN.md "Roofline").
+    pixels = pixels in flight; per-pixel-sample SoA records: hit 16 B, shading point 16 B,
+    shadow record 32 B per ray, rstate 4 B, queue entry 4 B, running sum 12 B (read + write)."""
+    spp = max(1, st.samples // max(1, pixels))
+    ps = pixels * spp
+    hits, shadow, draws = st.primary_hits, st.shadow_rays, st.rng_draws
+    return {
+        "wf_primary": ps * 16 + (st.rays - shadow - hits) * 24,      # hit record; light-only sum RMW (upper bound)
+        "wf_shade": ps * (16 + 8) + hits * (16 + 4) + shadow * 32 + draws * MT_BYTES_PER_DRAW,
+        "wf_shadow": shadow * (16 + 4 + 24 + 32),
+    }
+
+
+def roofline_of(stats, pixels, args, kernel_ms):
+    """Roofline of the dominant kernel: algorithmic bytes per launch / average launch duration
+    (HIP events on the render stream, recorded around every launch inside the timed region)."""
+    st = stats[-1]
+    n = len(stats)
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as fh:
+                tj = json.load(fh)
+            if tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if st.pipeline == 1:  # megakernel: one launch per frame
+        alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES
+        achieved = alg / (kernel_ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "sp_render_kernel",
+                "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg}
+    names = ["wf_init+wf_resolve", "wf_primary", "wf_shade", "wf_shadow"]
+    tot = [sum(s.stage_ms[k] for s in stats) / n for k in range(4)]
+    spp = args.spp
+    by = stage_bytes(st, pixels)
+    stages = {}
+    for k in (1, 2, 3):
+        ms_launch = tot[k] / spp
+        b_launch = by[names[k]] / spp
+        stages[names[k]] = {"ms_per_launch": round(ms_launch, 4), "frame_ms": round(tot[k], 2),
+                            "alg_bytes_per_launch": b_launch,
+                            "gbs": round(b_launch / max(ms_launch, 1e-9) / 1e6, 1)}
+    stages[names[0]] = {"frame_ms": round(tot[0], 3)}
+    dom = max((1, 2, 3), key=lambda k: tot[k])
+    d = stages[names[dom]]
+    achieved = d["gbs"]
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": names[dom],
+            "kernel_ms": d["ms_per_launch"], "alg_bytes_per_launch": d["alg_bytes_per_launch"],
+            "frame_kernel_ms": round(kernel_ms, 2), "stages": stages}
 
 
 def cpu_baseline(scene, integ, args, gpu_out, my_tiles):

@@ -164,8 +164,16 @@ typedef struct sp_render_params {
     int64_t        num_tiles;         /* length of tile_ids (ignored when tile_ids == NULL)      */
     void*          stream;            /* hipStream_t, NULL = default stream                      */
     int32_t        bvh_mode;          /* 0 = SAH (fast), 1 = reference median-split order        */
-    int32_t        flags;             /* reserved                                                 */
+    int32_t        flags;             /* SP_PIPELINE_* (0 = automatic)                            */
 } sp_render_params;
+
+/* Device pipeline selection (sp_render_params.flags).  Both produce identical images. */
+enum {
+    SP_PIPELINE_AUTO       = 0, /* wavefront where available (DirectLighting), else megakernel  */
+    SP_PIPELINE_MEGAKERNEL = 1, /* one lane owns one pixel for all samples (sp_mega.hpp)        */
+    SP_PIPELINE_WAVEFRONT  = 2, /* per-sample primary/shade/shadow kernels (sp_wave.hip)        */
+    SP_RENDER_STAGE_TIMING = 4  /* flag: HIP events between launches fill sp_render_stats.stage_ms */
+};
 
 typedef struct sp_render_stats {
     uint64_t rays;            /* every ray cast: camera/extension + shadow + MIS rays            */
@@ -173,7 +181,11 @@ typedef struct sp_render_stats {
     uint64_t samples;         /* pixel samples (paths)                                            */
     uint64_t rng_draws;       /* IncoherentSampler draws                                          */
     float    kernel_ms;       /* HIP-event time of the render kernel(s)                           */
-    float    twist_ms;        /* reserved                                                         */
+    int32_t  pipeline;        /* SP_PIPELINE_* that ran                                           */
+    int32_t  launches;        /* kernel launches issued                                           */
+    uint64_t primary_hits;    /* wavefront: camera rays that hit geometry (shading work items)     */
+    float    stage_ms[4];     /* with SP_RENDER_STAGE_TIMING, wavefront: [init+resolve, primary,   */
+                              /* shade, shadow] summed over launches; megakernel: [0] = kernel     */
 } sp_render_stats;
 
 /* ---- API ------------------------------------------------------------------------------ */

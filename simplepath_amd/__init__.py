@@ -44,6 +44,10 @@ class RenderStats:
     samples: int
     rng_draws: int
     kernel_ms: float
+    pipeline: int = 0
+    launches: int = 0
+    primary_hits: int = 0
+    stage_ms: tuple = (0.0, 0.0, 0.0, 0.0)
 
 
 class Scene:
@@ -149,7 +153,12 @@ class ColumnMajorTileScheduler(TileScheduler):
         return np.arange(rank, self.get_num_tiles(), world, dtype=np.int32)
 
 
-def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None) -> tuple:
+PIPELINES = {"auto": 0, "megakernel": 1, "wavefront": 2}
+STAGE_TIMING = 4  # SP_RENDER_STAGE_TIMING
+
+
+def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeline="auto",
+            stage_timing=False) -> tuple:
     if isinstance(integrator, str):
         integrator = string_to_integrator_type(integrator)
     p = _abi.sp_render_params()
@@ -161,16 +170,20 @@ def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None) -> tup
         p.tile_ids = keep.ctypes.data_as(C.POINTER(C.c_int32))
         p.num_tiles = keep.size
     p.stream = stream
+    p.flags = (PIPELINES[pipeline] if isinstance(pipeline, str) else int(pipeline)) | (STAGE_TIMING if stage_timing else 0)
     return p, keep
 
 
 def _stats(s: _abi.sp_render_stats) -> RenderStats:
-    return RenderStats(s.rays, s.shadow_rays, s.samples, s.rng_draws, s.kernel_ms)
+    return RenderStats(s.rays, s.shadow_rays, s.samples, s.rng_draws, s.kernel_ms, s.pipeline, s.launches,
+                       s.primary_hits, tuple(s.stage_ms))
 
 
-def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Optional[Sequence[int]] = None):
+def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Optional[Sequence[int]] = None,
+                 pipeline="auto"):
     """Render tiles on the GPU; returns (tile-packed radiance [n,64,3] float32, RenderStats)."""
-    p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids))
+    p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids),
+                      pipeline=pipeline)
     n = keep.size if keep is not None else TileScheduler(scene.width, scene.height).get_num_tiles()
     out = np.zeros((max(n, 1), 64, 3), dtype=np.float32)
     st = _abi.sp_render_stats()
@@ -178,9 +191,11 @@ def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Opt
     return out[:n], _stats(st)
 
 
-def render_tiles_device(scene: Scene, integrator, num_pixel_samples: int, tile_ids, out_ptr: int, stream=None):
+def render_tiles_device(scene: Scene, integrator, num_pixel_samples: int, tile_ids, out_ptr: int, stream=None,
+                        pipeline="auto", stage_timing=False):
     """Render into a caller-owned device buffer (e.g. a torch.cuda tensor's data_ptr())."""
-    p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids), stream)
+    p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids), stream,
+                      pipeline, stage_timing)
     st = _abi.sp_render_stats()
     check(lib().sp_render_tiles(scene.handle, C.byref(p), C.c_void_p(out_ptr), C.byref(st)))
     return _stats(st)

@@ -1,5 +1,6 @@
 // sp_capi.hip -- extern "C" boundary (include/simplepath_hip.h) and HBM residency of scenes.
 #include "sp_device.hpp"
+#include "sp_wave.hpp"
 #include "../host/sp_host.hpp"
 
 #include <hip/hip_runtime.h>
@@ -30,7 +31,7 @@ int fail(int code, const std::string& msg)
         if (e__ != hipSuccess) return fail(SP_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e__)); \
     } while (0)
 
-constexpr int MAX_RECURSION = 32; // sp_render.hip integrate_bruteforce / integrate_whitted
+constexpr int MAX_RECURSION = 32; // sp_path.hpp integrate_bruteforce / integrate_whitted
 
 uint32_t code_of(int kind, int index) { return ((uint32_t)kind << spd::CODE_SHIFT) | (uint32_t)index; }
 
@@ -110,6 +111,10 @@ struct sp_scene {
     unsigned long long*  counters     = nullptr;
     int32_t*             d_tiles      = nullptr;
     size_t               d_tiles_cap  = 0;
+    void*                wave_buf     = nullptr; // wavefront pipeline state (sp_wave.hpp WaveArgs)
+    size_t               wave_cap     = 0;
+    std::vector<hipEvent_t> stage_ev;            // SP_RENDER_STAGE_TIMING
+    int                  n_cu         = 0;
     hipEvent_t           ev0 = nullptr, ev1 = nullptr;
 
     void release()
@@ -121,6 +126,11 @@ struct sp_scene {
         if (tile_counter) (void)hipFree(tile_counter);
         if (counters) (void)hipFree(counters);
         if (d_tiles) (void)hipFree(d_tiles);
+        if (wave_buf) (void)hipFree(wave_buf);
+        wave_buf = nullptr;
+        wave_cap = 0;
+        for (hipEvent_t e : stage_ev) (void)hipEventDestroy(e);
+        stage_ev.clear();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
@@ -467,7 +477,7 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     s->geom_slots  = slot_code.size();
     d.stack_depth  = std::max(bvh.max_depth, lbvh.max_depth) + 1;
     SP_HIP(hipMalloc(&s->tile_counter, sizeof(int32_t)));
-    SP_HIP(hipMalloc(&s->counters, 4 * sizeof(unsigned long long)));
+    SP_HIP(hipMalloc(&s->counters, 8 * sizeof(unsigned long long)));
     SP_HIP(hipEventCreate(&s->ev0));
     SP_HIP(hipEventCreate(&s->ev1));
     return SP_OK;
@@ -505,42 +515,137 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         }
         SP_HIP(hipMemcpyAsync(s->d_tiles, p->tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream));
     }
-    const int    rs_words  = 2 << s->dev.rsqrt_bits;
-    const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_depth * 64 * 4;
-    if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
-    hipDeviceProp_t prop;
-    SP_HIP(hipGetDeviceProperties(&prop, s->device));
-    int variant = 0;
-    if (const char* v = std::getenv("SP_KERNEL_VARIANT")) variant = std::atoi(v);
-    const int     per_cu  = spd::render_blocks_per_cu(integ, variant, lds_bytes);
-    const int64_t max_blk = (int64_t)prop.multiProcessorCount * per_cu;
-    const int64_t need    = (n_tiles + 3) / 4;
-    const int     blocks  = (int)std::max<int64_t>(1, std::min(max_blk, need));
-    const size_t  waves   = (size_t)blocks * 4;
-    if (waves > s->mt_waves) {
-        if (s->mt_state) (void)hipFree(s->mt_state);
-        s->mt_state = nullptr;
-        SP_HIP(hipMalloc(&s->mt_state, waves * 2 * spm::MT_N * 64 * sizeof(uint64_t)));
-        s->mt_waves = waves;
+    if (s->n_cu == 0) {
+        hipDeviceProp_t prop;
+        SP_HIP(hipGetDeviceProperties(&prop, s->device));
+        s->n_cu = prop.multiProcessorCount;
     }
-    SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
-    SP_HIP(hipMemsetAsync(s->counters, 0, 4 * sizeof(unsigned long long), stream));
-    spd::RenderArgs a{};
-    a.out          = d_out;
-    a.tile_ids     = p->tile_ids ? s->d_tiles : nullptr;
-    a.num_tiles    = n_tiles;
-    a.tiles_x      = (s->dev.width + 7) / 8;
-    a.spp          = p->samples_per_pixel;
-    a.integrator   = integ;
-    a.tile_counter = s->tile_counter;
-    a.mt_state     = s->mt_state;
-    a.counters     = s->counters;
-    SP_HIP(hipEventRecord(s->ev0, stream));
-    SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
+    const bool timing   = (p->flags & SP_RENDER_STAGE_TIMING) != 0;
+    float      stage[4] = { 0, 0, 0, 0 };
+    int pipeline = p->flags & 3;
+    if (pipeline == 3) return fail(SP_ERR_ARG, "unknown pipeline flag");
+    const bool wave_ok = integ == SP_INTEGRATOR_DIRECT_LIGHTING && s->dev.n_lights <= spd::WF_MAX_LIGHTS;
+    if (pipeline == SP_PIPELINE_WAVEFRONT && !wave_ok)
+        return fail(SP_ERR_UNSUPPORTED, "wavefront pipeline supports DirectLighting with <= 32 lights");
+    if (pipeline == SP_PIPELINE_AUTO) pipeline = wave_ok ? SP_PIPELINE_WAVEFRONT : SP_PIPELINE_MEGAKERNEL;
+    SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
+    int launches = 0;
+    if (pipeline == SP_PIPELINE_WAVEFRONT) {
+        const size_t stack_lds = (size_t)4 * s->dev.stack_depth * 64 * 4;
+        if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+        // Pixels in flight per pass: all requested tiles unless the state would exceed the budget
+        // (SP_WAVE_MAX_GB, default 64 GB of the 288 GB HBM); larger jobs run in tile chunks.
+        double budget_gb = 64.0;
+        if (const char* v = std::getenv("SP_WAVE_MAX_GB")) budget_gb = std::atof(v);
+        const size_t  per_pix   = spd::wave_bytes_per_pixel(s->dev.n_lights);
+        const int64_t max_tiles = std::max<int64_t>(1, (int64_t)(budget_gb * 1e9 / (double)(per_pix * 64)));
+        const int64_t chunk     = std::min<int64_t>(n_tiles, max_tiles);
+        const size_t  n         = (size_t)chunk * 64;
+        const size_t  need      = n * per_pix + 256 * 8;
+        if (need > s->wave_cap) {
+            if (s->wave_buf) (void)hipFree(s->wave_buf);
+            s->wave_buf = nullptr;
+            s->wave_cap = 0;
+            SP_HIP(hipMalloc(&s->wave_buf, need));
+            s->wave_cap = need;
+        }
+        // carve: every array 256-byte aligned (n is a multiple of 64)
+        char* b    = static_cast<char*>(s->wave_buf);
+        auto  take = [&](size_t bytes) { char* r = b; b += (bytes + 255) & ~(size_t)255; return r; };
+        spd::WaveArgs w{};
+        w.n        = (int64_t)n;
+        w.tiles_x  = (s->dev.width + 7) / 8;
+        w.spp      = p->samples_per_pixel;
+        w.mt_state = reinterpret_cast<uint64_t*>(take(n * 2 * spm::MT_N * 8));
+        w.sh       = reinterpret_cast<float4*>(take(n * (size_t)std::max(1, s->dev.n_lights) * 32));
+        w.hit      = reinterpret_cast<float4*>(take(n * 16));
+        w.shp      = reinterpret_cast<float4*>(take(n * 16));
+        w.acc      = reinterpret_cast<float*>(take(n * 12));
+        w.rstate   = reinterpret_cast<uint32_t*>(take(n * 4));
+        w.queue    = reinterpret_cast<uint32_t*>(take(n * 4));
+        w.qcount   = reinterpret_cast<uint32_t*>(take(256));
+        w.counters = s->counters;
+        const int per_cu = spd::wave_traverse_blocks_per_cu(s->dev);
+        const size_t n_ev = timing ? 3 * (size_t)w.spp + 3 : 0;
+        while (s->stage_ev.size() < n_ev) {
+            hipEvent_t e;
+            SP_HIP(hipEventCreate(&e));
+            s->stage_ev.push_back(e);
+        }
+        SP_HIP(hipEventRecord(s->ev0, stream));
+        for (int64_t t0 = 0; t0 < n_tiles; t0 += chunk) {
+            const int64_t nt = std::min<int64_t>(chunk, n_tiles - t0);
+            w.n        = nt * 64;
+            w.tile_ids = p->tile_ids ? s->d_tiles + t0 : nullptr;
+            if (!p->tile_ids && t0 > 0) {
+                // identity ids beyond the first chunk: materialise them
+                std::vector<int32_t> ids((size_t)nt);
+                for (int64_t i = 0; i < nt; ++i) ids[(size_t)i] = (int32_t)(t0 + i);
+                if ((size_t)nt > s->d_tiles_cap) {
+                    if (s->d_tiles) (void)hipFree(s->d_tiles);
+                    s->d_tiles = nullptr;
+                    SP_HIP(hipMalloc(&s->d_tiles, (size_t)chunk * sizeof(int32_t)));
+                    s->d_tiles_cap = (size_t)chunk;
+                }
+                SP_HIP(hipMemcpyAsync(s->d_tiles, ids.data(), (size_t)nt * 4, hipMemcpyHostToDevice, stream));
+                SP_HIP(hipStreamSynchronize(stream));
+                w.tile_ids = s->d_tiles;
+            }
+            SP_HIP(spd::wave_render(s->dev, w, d_out + (size_t)t0 * 64 * 3, per_cu, s->n_cu, stream,
+                                    timing ? s->stage_ev.data() : nullptr));
+            launches += 2 + 3 * (int)w.spp;
+            if (timing) {
+                SP_HIP(hipEventSynchronize(s->stage_ev[n_ev - 1]));
+                auto el = [&](size_t a, size_t b) {
+                    float ms = 0.0f;
+                    (void)hipEventElapsedTime(&ms, s->stage_ev[a], s->stage_ev[b]);
+                    return ms;
+                };
+                stage[0] += el(0, 1) + el(n_ev - 2, n_ev - 1);
+                for (uint32_t i = 0; i < w.spp; ++i) {
+                    const size_t b = 1 + 3 * (size_t)i;
+                    stage[1] += el(b, b + 1);
+                    stage[2] += el(b + 1, b + 2);
+                    stage[3] += el(b + 2, b + 3);
+                }
+            }
+        }
+    } else {
+        const int    rs_words  = 2 << s->dev.rsqrt_bits;
+        const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_depth * 64 * 4;
+        if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+        int variant = 0;
+        if (const char* v = std::getenv("SP_KERNEL_VARIANT")) variant = std::atoi(v);
+        const int     per_cu  = spd::render_blocks_per_cu(integ, variant, lds_bytes);
+        const int64_t max_blk = (int64_t)s->n_cu * per_cu;
+        const int64_t need    = (n_tiles + 3) / 4;
+        const int     blocks  = (int)std::max<int64_t>(1, std::min(max_blk, need));
+        const size_t  waves   = (size_t)blocks * 4;
+        if (waves > s->mt_waves) {
+            if (s->mt_state) (void)hipFree(s->mt_state);
+            s->mt_state = nullptr;
+            SP_HIP(hipMalloc(&s->mt_state, waves * 2 * spm::MT_N * 64 * sizeof(uint64_t)));
+            s->mt_waves = waves;
+        }
+        SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
+        spd::RenderArgs a{};
+        a.out          = d_out;
+        a.tile_ids     = p->tile_ids ? s->d_tiles : nullptr;
+        a.num_tiles    = n_tiles;
+        a.tiles_x      = (s->dev.width + 7) / 8;
+        a.spp          = p->samples_per_pixel;
+        a.integrator   = integ;
+        a.tile_counter = s->tile_counter;
+        a.mt_state     = s->mt_state;
+        a.counters     = s->counters;
+        SP_HIP(hipEventRecord(s->ev0, stream));
+        SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
+        launches = 1;
+    }
     SP_HIP(hipEventRecord(s->ev1, stream));
     SP_HIP(hipEventSynchronize(s->ev1));
     if (stats) {
-        unsigned long long c[4];
+        unsigned long long c[8];
         SP_HIP(hipMemcpy(c, s->counters, sizeof(c), hipMemcpyDeviceToHost));
         float ms = 0.0f;
         SP_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -549,7 +654,11 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         stats->samples     = c[2];
         stats->rng_draws   = c[3];
         stats->kernel_ms   = ms;
-        stats->twist_ms    = (float)blocks; // diagnostic: persistent blocks launched
+        stats->pipeline    = pipeline;
+        stats->launches    = launches;
+        stats->primary_hits = c[4];
+        if (pipeline == SP_PIPELINE_MEGAKERNEL && timing) stage[0] = ms;
+        for (int k = 0; k < 4; ++k) stats->stage_ms[k] = stage[k];
     }
     return SP_OK;
 }

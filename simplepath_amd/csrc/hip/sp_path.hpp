@@ -1,4 +1,4 @@
-// sp_render.hip -- per-pixel path integration on gfx950 (MI355X), bit-exact with the reference.
+// sp_path.hpp -- device implementation of the reference's per-pixel path (gfx950), bit-exact.
 //
 // One 64-lane wave renders one 8x8 tile (base/Tile.h:10 k_tile_dimension = 8), lane = Morton
 // index inside the tile (base/Tile.h TilePixelIterator), exactly the pixel order of
@@ -12,6 +12,7 @@
 //
 // Numerics: every float operation follows the reference's order; FMAs only where the reference
 // issues them (sp_math.h).  Build flags: -ffp-contract=off, IEEE division/sqrt, denormals kept.
+#pragma once
 #include "sp_device.hpp"
 
 namespace spd {
@@ -1267,137 +1268,4 @@ __device__ __forceinline__ uint32_t morton_decode_1(uint32_t a)
     return a;
 }
 
-constexpr int WAVES_PER_BLOCK = 4;
-
-template <int INTEG>
-__device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
-{
-    if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE) return integrate_bruteforce(c, ray);
-    else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE) return integrate_iterative<false>(c, ray);
-    else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR) return integrate_iterative<true>(c, ray);
-    else if constexpr (INTEG == SP_INTEGRATOR_ITERATIVE_RRNEE) return integrate_rrnee(c, ray);
-    else if constexpr (INTEG == SP_INTEGRATOR_WHITTED) return integrate_whitted(c, ray);
-    else return integrate_direct(c, ray);
-}
-
-// Persistent kernel: 4 waves per block share the LDS RSQRTSS table; each wave independently
-// pulls 8x8 tiles from the queue (TileScheduler::get_next_tile) and owns one MT state slot.
-// One instantiation per integrator so each carries only its own live state; MINW is the
-// __launch_bounds__ occupancy request (waves per SIMD) chosen by measurement.
-template <int INTEG, int MINW>
-__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(Scene sc, RenderArgs args)
-{
-    extern __shared__ uint32_t lds[];
-    const int tid  = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int rs_words = 2 << sc.rsqrt_bits;
-    for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
-    __syncthreads();
-    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
-    Stack st{ lds + rs_words + wave * sc.stack_depth * 64, lane };
-
-    const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;
-    Rng          rng;
-    rng.base = args.mt_state + gwave * (2 * MT_N * 64) + lane;
-
-    uint32_t rays_total = 0, shadow_total = 0, samples_total = 0, draws_total = 0;
-    const uint32_t dx = morton_decode_1((uint32_t)lane);
-    const uint32_t dy = morton_decode_1((uint32_t)lane >> 1);
-    while (true) {
-        int grabbed = 0;
-        if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
-        const int64_t slot = __shfl(grabbed, 0, 64);
-        if (slot >= args.num_tiles) break;
-        const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
-        const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
-        const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
-        const bool     inside = (int)px < sc.width && (int)py < sc.height;
-        rgb            acc    = mkc(0, 0, 0);
-        if (inside) {
-            const uint32_t pix_seed = (px << 16u) | py;
-            rng_seed(rng, pix_seed ^ 0xb0ae9d99u);          // get_integrator_sampler (main.cpp:73)
-            const uint32_t seed2d = pix_seed ^ 0x6184faf4u; // RSequenceSampler m_seed_2D (main.cpp:67)
-            Ctx c{ sc, rng, q, st, 0u, 0u };
-            for (uint32_t i = 0; i < args.spp; ++i) {
-                rng_prepare(rng);
-                // RSequenceSampler::get_next_2D (math/Sampler.h:158) with count i
-                const float sx = rseq_component(seed2d, sc.alpha2_0, i);
-                const float sy = rseq_component(seed2d, sc.alpha2_1, i);
-                const float fx = (float)(int)px + sx;
-                const float fy = (float)(int)py + sy;
-                // PerspectiveCamera::generate_ray_impl (Cameras/Camera.h:119)
-                Ray ray;
-                ray.o = sc.camera.p;
-                ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
-                acc   = cadd(acc, integrate<INTEG>(c, ray)); // image(p) += integrate(...)
-            }
-            acc = cdivs(acc, (float)args.spp); // image(p) /= num_pixel_samples
-            rays_total += c.rays;
-            shadow_total += c.shadow;
-            samples_total += args.spp;
-            draws_total += rng.draws;
-        }
-        float* o = args.out + ((size_t)slot * 64 + lane) * 3;
-        o[0]     = acc.r;
-        o[1]     = acc.g;
-        o[2]     = acc.b;
-    }
-    unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
-    for (int k = 0; k < 4; ++k) {
-        unsigned long long s = v[k];
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
-        if (lane == 0 && s) atomicAdd(args.counters + k, s);
-    }
-}
-
-} // namespace spd
-
-// ============================================================================ host launch helpers
-namespace spd {
-using KernelFn = void (*)(Scene, RenderArgs);
-
-template <int MINW>
-KernelFn kernel_for(int integ)
-{
-    if constexpr (MINW != 2) {
-        if (integ == SP_INTEGRATOR_DIRECT_LIGHTING) return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, MINW>;
-        return kernel_for<2>(integ);
-    }
-    switch (integ) {
-    case SP_INTEGRATOR_BRUTE_FORCE: return sp_render_kernel<SP_INTEGRATOR_BRUTE_FORCE, MINW>;
-    case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE: return sp_render_kernel<SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE, MINW>;
-    case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: return sp_render_kernel<SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR, MINW>;
-    case SP_INTEGRATOR_ITERATIVE_RRNEE: return sp_render_kernel<SP_INTEGRATOR_ITERATIVE_RRNEE, MINW>;
-    case SP_INTEGRATOR_WHITTED: return sp_render_kernel<SP_INTEGRATOR_WHITTED, MINW>;
-    default: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, MINW>;
-    }
-}
-
-// variant = requested waves per SIMD for __launch_bounds__ (1..4); 0 = default choice
-KernelFn select_kernel(int integ, int variant)
-{
-    switch (variant) {
-    case 1: return kernel_for<1>(integ);
-    case 3: return kernel_for<3>(integ);
-    case 4: return kernel_for<4>(integ);
-    default: return kernel_for<2>(integ);
-    }
-}
-
-hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
-                         hipStream_t stream)
-{
-    hipLaunchKernelGGL(select_kernel(integ, variant), dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);
-    return hipGetLastError();
-}
-
-int render_blocks_per_cu(int integ, int variant, size_t lds_bytes)
-{
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_kernel(integ, variant), 64 * WAVES_PER_BLOCK, lds_bytes) !=
-        hipSuccess)
-        return 1;
-    return n > 0 ? n : 1;
-}
 } // namespace spd

@@ -1,0 +1,33 @@
+// sp_wave.hpp -- arguments and host entry points of the wavefront pipeline (sp_wave.hip).
+#pragma once
+#include "sp_device.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace spd {
+
+struct WaveArgs {
+    int64_t             n;         // pixel slots in flight = tiles * 64
+    const int32_t*      tile_ids;  // nullptr => identity
+    int32_t             tiles_x;
+    uint32_t            spp;
+    float*              acc;       // [3][n]
+    uint32_t*           rstate;    // [n]
+    float4*             hit;       // [n]
+    float4*             shp;       // [n]
+    float4*             sh;        // [n_lights][n][2]
+    uint32_t*           queue;     // [n]
+    uint32_t*           qcount;
+    uint64_t*           mt_state;  // [n/64][2][312][64]
+    unsigned long long* counters;  // [rays, shadow_rays, samples, draws, primary_hits]
+};
+
+constexpr int WF_MAX_LIGHTS = 32; // light mask is one u32 per pixel
+
+size_t     wave_bytes_per_pixel(int n_lights);
+// ev: optional 3 * spp + 3 events recorded around every launch (stage timing)
+hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
+                       hipStream_t stream, hipEvent_t* ev);
+int        wave_traverse_blocks_per_cu(const Scene& sc);
+
+} // namespace spd

@@ -30,9 +30,11 @@ def load(scene_dir, name, w, h, bvh):
     return s
 
 
-def test_bunny_direct_lighting_bitexact(scene_dir):
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+def test_bunny_direct_lighting_bitexact(scene_dir, pipeline):
     s = load(scene_dir, "bunny.sp", 64, 40, bvh=1)
-    g, gst = sp.render_tiles(s, "direct_lighting", 4)
+    g, gst = sp.render_tiles(s, "direct_lighting", 4, pipeline=pipeline)
+    assert gst.pipeline == sp.PIPELINES[pipeline]
     c, cst = _oracle.render(s, 6, 4, variant="spm")
     assert gst.samples == cst["samples"] == 64 * 40 * 4
     assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
@@ -87,3 +89,34 @@ def test_vs_glibc_oracle_bitexact(scene_dir, integrator):
     frac = float(np.mean(np.all(g == c, axis=-1)))
     print(f"GPU vs glibc-libm oracle ({integrator}): rel_l2={r:.3e} bitexact_pixels={frac:.4f}")
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+
+
+@pytest.mark.parametrize("scene,bvh", [("bunny.sp", 0), ("material_spheres.sp", 1)])
+def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
+    # the two device pipelines run the same floating-point sequence per pixel
+    s = load(scene_dir, scene, 72, 40, bvh=bvh)
+    m, mst = sp.render_tiles(s, "direct_lighting", 5, pipeline="megakernel")
+    w, wst = sp.render_tiles(s, "direct_lighting", 5, pipeline="wavefront")
+    assert np.array_equal(m.view(np.uint32), w.view(np.uint32)), rel_l2(w, m)
+    assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
+        (wst.rays, wst.shadow_rays, wst.samples, wst.rng_draws)
+    assert wst.launches == 2 + 3 * 5 and mst.launches == 1
+
+
+def test_wavefront_tile_chunks(scene_dir, monkeypatch):
+    # a tiny state budget forces several tile chunks per call; result must not change
+    s = load(scene_dir, "bunny.sp", 64, 48, bvh=0)
+    ids = np.arange(sp.TileScheduler(64, 48).get_num_tiles() - 1, -1, -1, dtype=np.int32)
+    ref, _ = sp.render_tiles(s, "direct_lighting", 3, ids, pipeline="wavefront")
+    monkeypatch.setenv("SP_WAVE_MAX_GB", "0.0016")  # ~5 tiles per chunk
+    a, ast = sp.render_tiles(s, "direct_lighting", 3, ids, pipeline="wavefront")
+    b, _ = sp.render_tiles(s, "direct_lighting", 3, None, pipeline="wavefront")
+    assert ast.launches > 2 + 3 * 3
+    assert np.array_equal(a, ref)
+    assert np.array_equal(b[ids], ref)
+
+
+def test_wavefront_rejects_other_integrators(scene_dir):
+    s = load(scene_dir, "bunny.sp", 16, 16, bvh=0)
+    with pytest.raises(sp.SimplePathError):
+        sp.render_tiles(s, "iterative_rrnee", 1, pipeline="wavefront")
