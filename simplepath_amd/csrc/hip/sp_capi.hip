@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -476,6 +477,10 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     s->geom_nodes  = nodes.size();
     s->geom_slots  = slot_code.size();
     d.stack_depth  = std::max(bvh.max_depth, lbvh.max_depth) + 1;
+    d.packet       = d.stack_depth <= 64 ? 1 : 0; // sp_packet.hpp PACKET_MAX_DEPTH
+    d.ordered      = bvh_mode == 1 ? 0 : 1;       // reference order is part of the bit-exact contract
+    if (const char* v = std::getenv("SP_PACKET")) d.packet = d.packet && std::atoi(v) != 0;
+    if (const char* v = std::getenv("SP_ORDERED")) d.ordered = d.ordered && std::atoi(v) != 0;
     SP_HIP(hipMalloc(&s->tile_counter, sizeof(int32_t)));
     SP_HIP(hipMalloc(&s->counters, 8 * sizeof(unsigned long long)));
     SP_HIP(hipEventCreate(&s->ev0));
@@ -541,7 +546,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         const int64_t max_tiles = std::max<int64_t>(1, (int64_t)(budget_gb * 1e9 / (double)(per_pix * 64)));
         const int64_t chunk     = std::min<int64_t>(n_tiles, max_tiles);
         const size_t  n         = (size_t)chunk * 64;
-        const size_t  need      = n * per_pix + 256 * 8;
+        const size_t  need      = n * per_pix + spd::wave_stat_bytes((int64_t)n) + spd::wave_queue_bytes((int64_t)n) + 256 * 10;
         if (need > s->wave_cap) {
             if (s->wave_buf) (void)hipFree(s->wave_buf);
             s->wave_buf = nullptr;
@@ -562,9 +567,19 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         w.shp      = reinterpret_cast<float4*>(take(n * 16));
         w.acc      = reinterpret_cast<float*>(take(n * 12));
         w.rstate   = reinterpret_cast<uint32_t*>(take(n * 4));
-        w.queue    = reinterpret_cast<uint32_t*>(take(n * 4));
-        w.qcount   = reinterpret_cast<uint32_t*>(take(256));
+        w.queue    = reinterpret_cast<uint32_t*>(take(spd::wave_queue_bytes((int64_t)n)));
+        w.qcount   = w.queue + (spd::wave_queue_bytes((int64_t)n) / 4 - 32 * 32);
+        w.wstat    = reinterpret_cast<unsigned long long*>(take(spd::wave_stat_bytes((int64_t)n)));
         w.counters = s->counters;
+        // SP_WAVE_DIAG=<file>: per-wave timeline of one sample's primary + shadow launches
+        const char*         diag_path = std::getenv("SP_WAVE_DIAG");
+        unsigned long long* d_diag    = nullptr;
+        const size_t        diag_n    = 2 * (n / 64) * 4;
+        if (diag_path) {
+            SP_HIP(hipMalloc(&d_diag, diag_n * 8));
+            SP_HIP(hipMemsetAsync(d_diag, 0, diag_n * 8, stream));
+        }
+        w.diag = d_diag;
         const int per_cu = spd::wave_traverse_blocks_per_cu(s->dev);
         const size_t n_ev = timing ? 3 * (size_t)w.spp + 3 : 0;
         while (s->stage_ev.size() < n_ev) {
@@ -593,7 +608,19 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
             }
             SP_HIP(spd::wave_render(s->dev, w, d_out + (size_t)t0 * 64 * 3, per_cu, s->n_cu, stream,
                                     timing ? s->stage_ev.data() : nullptr));
-            launches += 2 + 3 * (int)w.spp;
+            launches += 3 + 3 * (int)w.spp;
+            if (d_diag) {
+                std::vector<unsigned long long> h(diag_n);
+                SP_HIP(hipStreamSynchronize(stream));
+                SP_HIP(hipMemcpy(h.data(), d_diag, diag_n * 8, hipMemcpyDeviceToHost));
+                if (FILE* f = std::fopen(diag_path, "wb")) {
+                    std::fwrite(h.data(), 8, diag_n, f);
+                    std::fclose(f);
+                }
+                (void)hipFree(d_diag);
+                d_diag = nullptr;
+                w.diag = nullptr;
+            }
             if (timing) {
                 SP_HIP(hipEventSynchronize(s->stage_ev[n_ev - 1]));
                 auto el = [&](size_t a, size_t b) {

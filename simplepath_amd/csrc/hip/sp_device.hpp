@@ -23,6 +23,8 @@ using spm::rgb;
 constexpr uint32_t LEAF_BIT   = 0x80000000u;
 constexpr uint32_t CODE_SHIFT = 30;
 constexpr uint32_t CODE_MASK  = (1u << CODE_SHIFT) - 1u;
+constexpr uint32_t AXIS_SHIFT = 30;                      // sp_host.hpp BVH_AXIS_SHIFT
+constexpr uint32_t CHILD_MASK = (1u << AXIS_SHIFT) - 1u;
 
 struct Node {
     float    lo[3];
@@ -86,6 +88,8 @@ struct Scene {
     int32_t         rsqrt_bits;
     uint32_t        rsqrt_zero, rsqrt_denorm;
     int             stack_depth;   // LDS traversal stack entries per lane
+    int             packet;        // 1: BVHs shallow enough for the wave-coherent walk (sp_packet.hpp)
+    int             ordered;       // 1: SAH BVH -- visit the near child (split axis, ray sign) first
 };
 
 struct RenderArgs {

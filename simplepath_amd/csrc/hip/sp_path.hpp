@@ -308,6 +308,16 @@ struct Stack {
     int       lane;
 };
 
+// SAH nodes carry their split axis: the child on the far side of the ray's direction goes on
+// the stack.  Only the visiting order changes (closest hit: equal-distance ties may resolve to
+// another primitive; any hit: no change), so the reference-order BVH never uses it.
+__device__ __forceinline__ bool near_is_second(uint32_t a, const f3& d)
+{
+    const uint32_t ax = a >> AXIS_SHIFT;
+    const float    da = (ax == 0) ? d.x : ((ax == 1) ? d.y : d.z);
+    return da < 0.0f;
+}
+
 // Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
 __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
@@ -333,9 +343,11 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
                 const uint32_t cnt = n.b & ~LEAF_BIT;
                 for (uint32_t k = 0; k < cnt; ++k) prim_closest(sc, n.a + k, ray, tmin, h);
             } else {
-                st.s[sp * 64 + st.lane] = n.b; // child 1 deferred
+                uint32_t first = n.a & CHILD_MASK, second = n.b; // reference: child 0 first
+                if (sc.ordered && near_is_second(n.a, ray.d)) { const uint32_t t = first; first = second; second = t; }
+                st.s[sp * 64 + st.lane] = second; // deferred, box tested when popped
                 ++sp;
-                cur      = n.a;                 // child 0 next
+                cur      = first;
                 test_box = true;
                 continue;
             }
@@ -369,9 +381,11 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
                 for (uint32_t k = 0; k < cnt; ++k)
                     if (prim_any(sc, n.a + k, ray, tmin, tmax)) return true;
             } else {
-                st.s[sp * 64 + st.lane] = n.b;
+                uint32_t first = n.a & CHILD_MASK, second = n.b;
+                if (sc.ordered && near_is_second(n.a, ray.d)) { const uint32_t t = first; first = second; second = t; }
+                st.s[sp * 64 + st.lane] = second;
                 ++sp;
-                cur      = n.a;
+                cur      = first;
                 test_box = true;
                 continue;
             }
@@ -428,7 +442,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
             } else {
                 st.s[sp * 64 + st.lane] = n.b;
                 ++sp;
-                cur      = n.a;
+                cur      = n.a & CHILD_MASK;
                 test_box = true;
                 continue;
             }
@@ -461,7 +475,7 @@ __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, floa
             } else {
                 st.s[sp * 64 + st.lane] = n.b;
                 ++sp;
-                cur      = n.a;
+                cur      = n.a & CHILD_MASK;
                 test_box = true;
                 continue;
             }

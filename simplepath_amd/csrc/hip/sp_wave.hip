@@ -26,12 +26,17 @@
 //   acc[3][n] f32 SoA | rstate[n] u32 {idx | cur<<16 | ready<<17} | hit[n] float4 {t, code,
 //   beta, gamma} | shp[n] float4 {p.xyz, light mask} | sh[light][n][2] float4 {wi.xyz, tmin},
 //   {contrib.rgb, tmax} | queue[n] u32 | mt[tile][buf][312][64] u64 (as in the megakernel).
-#include "sp_path.hpp"
+#include "sp_packet.hpp"
 #include "sp_wave.hpp"
+
+#include <cstdlib>
 
 namespace spd {
 
 constexpr int WF_BLOCK = 256;
+constexpr int QSEG     = 32; // shadow-queue segments (one counter each, QSTRIDE words apart)
+constexpr int QSTRIDE  = 32;
+__host__ __device__ inline size_t qseg_cap(int64_t n) { return (size_t)64 * (size_t)(((n >> 6) + QSEG - 1) / QSEG); }
 
 struct PixelRef {
     uint32_t px, py;
@@ -65,11 +70,30 @@ __device__ __forceinline__ Ray camera_ray(const Scene& sc, const PixelRef& pr, u
     return ray;
 }
 
-__device__ __forceinline__ void wave_count(unsigned long long* ctr, uint32_t v)
+// Statistics without same-address atomics: each wave adds its sums into its own slot of
+// WaveArgs::wstat (plain read-modify-write; a slot belongs to one wave per launch); wf_stats
+// reduces the slots once per frame.  32400 waves x 3 kernels x 256 samples of device-scope
+// atomics on one address would serialise at the memory side.
+enum { ST_RAYS = 0, ST_SHADOW = 1, ST_SAMPLES = 2, ST_DRAWS = 3, ST_HITS = 4, ST_N = 5 };
+__device__ __forceinline__ void wave_count(unsigned long long* slot, int k, uint32_t v)
 {
-    unsigned long long s = v;
+    uint32_t s = v;
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(ctr, s);
+    if ((threadIdx.x & 63) == 0 && s) slot[k] += s;
+}
+
+// Diagnostic per-wave record (only when WaveArgs::diag is set): {t0, t1 (s_memrealtime,
+// 100 MHz), node steps | active lanes << 32, HW_ID | XCC_ID << 32}.
+__device__ __forceinline__ void diag_record(unsigned long long* rec, uint64_t t0, uint32_t steps, uint32_t lanes)
+{
+    if ((threadIdx.x & 63) != 0) return;
+    const uint64_t t1  = __builtin_amdgcn_s_memrealtime();
+    const uint32_t hw  = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((16 - 1) << 11));
+    rec[0]             = t0;
+    rec[1]             = t1;
+    rec[2]             = (uint64_t)steps | ((uint64_t)lanes << 32);
+    rec[3]             = (uint64_t)hw | ((uint64_t)xcc << 32);
 }
 
 __device__ __forceinline__ Rng rng_load(const WaveArgs& w, int64_t p)
@@ -112,33 +136,48 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uin
     extern __shared__ uint32_t lds[];
     const int64_t p    = (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
     const int     lane = threadIdx.x & 63;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *w.qcount = 0u; // wf_shadow of the previous sample is done
+    if (blockIdx.x == 0 && threadIdx.x < QSEG) w.qcount[threadIdx.x * QSTRIDE] = 0u; // previous wf_shadow is done
     if (p >= w.n) return;
+    const uint64_t t0 = w.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t       steps = 0;
     const PixelRef pr = pixel_of(sc, w, p);
     float4         hrec = make_float4(0.0f, __uint_as_float(0xffffffffu), 0.0f, 0.0f);
     uint32_t       rays = 0, hits = 0;
-    if (pr.inside && sc.max_depth > 0) {
-        const Rsq   q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
-        const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_depth * 64, lane };
-        const Ray   ray = camera_ray(sc, pr, sample, q);
-        rays            = 1;
-        float          tmax = k_infinite;
-        const LightHit lh   = scene_intersect_lights(sc, ray, k_ray_epsilon, tmax, st);
-        if (lh.hit) tmax = lh.t;
-        const Hit h = scene_intersect(sc, ray, k_ray_epsilon, tmax, st);
-        if (h.code != 0xffffffffu) {
-            hrec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
-            hits = 1;
-        } else if (lh.hit) {
-            const rgb L = cadd(mkc(0, 0, 0), cmul(mkc(1, 1, 1), lh.L));
-            w.acc[p]           = w.acc[p] + L.r;
-            w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
-            w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
+    const bool     on   = pr.inside && sc.max_depth > 0;
+    if (sc.packet || on) {
+        const Rsq q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+        const Ray ray  = camera_ray(sc, pr, sample, q);
+        float     tmax = k_infinite;
+        LightHit  lh;
+        Hit       h;
+        if (sc.packet) { // whole wave together: camera rays of one tile are coherent
+            lh = scene_intersect_lights_w(sc, ray, k_ray_epsilon, tmax, on);
+            if (lh.hit) tmax = lh.t;
+            h = scene_intersect_w(sc, ray, k_ray_epsilon, tmax, on, w.diag ? &steps : nullptr);
+        } else {
+            const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_depth * 64, lane };
+            lh = scene_intersect_lights(sc, ray, k_ray_epsilon, tmax, st);
+            if (lh.hit) tmax = lh.t;
+            h = scene_intersect(sc, ray, k_ray_epsilon, tmax, st);
+        }
+        if (on) {
+            rays = 1;
+            if (h.code != 0xffffffffu) {
+                hrec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
+                hits = 1;
+            } else if (lh.hit) {
+                const rgb L = cadd(mkc(0, 0, 0), cmul(mkc(1, 1, 1), lh.L));
+                w.acc[p]           = w.acc[p] + L.r;
+                w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
+                w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
+            }
         }
     }
     w.hit[p] = hrec;
-    wave_count(w.counters + 0, rays);
-    wave_count(w.counters + 4, hits);
+    if (w.diag) diag_record(w.diag + (size_t)(p >> 6) * 4, t0, steps, (uint32_t)__popcll(__ballot(pr.inside)));
+    unsigned long long* slot = w.wstat + (size_t)(p >> 6) * ST_N;
+    wave_count(slot, ST_RAYS, rays);
+    wave_count(slot, ST_HITS, hits);
 }
 
 // Shading: direct_nee's sampling half (Integrator.cpp:287-296).
@@ -184,17 +223,20 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shade(Scene sc, WaveArgs w, uint3
         draws = rng.draws;
         rng_store(w, p, rng);
     }
-    // active-ray compaction: wave ballot + one atomic per wave, queue keeps pixel order in a wave
+    // active-ray compaction: wave ballot + prefix popcount, one atomic per wave on one of QSEG
+    // segment counters (tile slot % QSEG) so that no single address serialises the chip
     const unsigned long long ballot = __ballot(mask != 0);
     if (ballot) {
-        const int      lane   = threadIdx.x & 63;
-        const uint32_t total  = (uint32_t)__popcll(ballot);
-        uint32_t       base   = 0;
-        if (lane == 0) base = atomicAdd(w.qcount, total);
+        const int      lane  = threadIdx.x & 63;
+        const uint32_t total = (uint32_t)__popcll(ballot);
+        const uint32_t seg   = (uint32_t)(p >> 6) % QSEG;
+        uint32_t       base  = 0;
+        if (lane == 0) base = atomicAdd(w.qcount + seg * QSTRIDE, total);
         base = __shfl(base, 0, 64);
-        if (mask) w.queue[base + (uint32_t)__popcll(ballot & ((1ull << lane) - 1ull))] = (uint32_t)p;
+        if (mask)
+            w.queue[(size_t)seg * qseg_cap(w.n) + base + (uint32_t)__popcll(ballot & ((1ull << lane) - 1ull))] = (uint32_t)p;
     }
-    wave_count(w.counters + 3, draws);
+    wave_count(w.wstat + (size_t)(p >> 6) * ST_N, ST_DRAWS, draws);
 }
 
 // Shadow queries + accumulation: direct_nee's occlusion half (Integrator.cpp:297-300).
@@ -203,30 +245,62 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shadow(Scene sc, WaveArgs w)
     extern __shared__ uint32_t lds[];
     const int      lane  = threadIdx.x & 63;
     const Stack    st{ lds + (threadIdx.x >> 6) * sc.stack_depth * 64, lane };
-    const uint32_t count = *w.qcount;
+    // Segment j holds the shadow pixels of tile slots j, j + QSEG, ... in arrival order.  Virtual
+    // chunk v = 64 entries of segment v % QSEG starting at (v / QSEG) * 64: walking v in order
+    // visits the tiles roughly in image order, which keeps neighbouring waves' BVH nodes in cache.
+    const uint32_t segn   = lane < QSEG ? w.qcount[lane * QSTRIDE] : 0u;
+    uint32_t       maxn   = segn;
+    for (int off = 32; off > 0; off >>= 1) maxn = max(maxn, (uint32_t)__shfl_xor(maxn, off, 64));
+    const uint32_t n_virt = QSEG * ((maxn + 63) / 64);
+    const size_t   cap    = qseg_cap(w.n);
     uint32_t       shadow = 0;
-    for (uint32_t k = blockIdx.x * WF_BLOCK + threadIdx.x; k < count; k += gridDim.x * WF_BLOCK) {
-        const int64_t  p    = w.queue[k];
-        const float4   o    = w.shp[p];
+    const uint64_t t0     = w.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t       steps  = 0;
+    const uint32_t wave_g = (blockIdx.x * WF_BLOCK + threadIdx.x) >> 6;
+    for (uint32_t v = wave_g; v < n_virt; v += gridDim.x * (WF_BLOCK / 64)) {
+        const uint32_t j    = v % QSEG;
+        const uint32_t k    = (v / QSEG) * 64 + (uint32_t)lane;
+        const bool     live = k < (uint32_t)__shfl(segn, (int)j, 64);
+        const int64_t  p    = live ? (int64_t)w.queue[(size_t)j * cap + k] : 0;
+        float4         o    = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (live) o = w.shp[p];
         const uint32_t mask = __float_as_uint(o.w);
         rgb            L    = mkc(0, 0, 0);
-        for (uint32_t m = mask; m; m &= m - 1) {
-            const int     li = __ffs(m) - 1;
-            const float4* e  = w.sh + ((size_t)li * w.n + p) * 2;
-            const float4  d  = e[0];
-            const float4  c  = e[1];
-            Ray           r;
+        for (int li = 0; li < sc.n_lights; ++li) {
+            const bool on = live && ((mask >> li) & 1u);
+            if (!__any(on)) continue;
+            float4 d = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (on) {
+                const float4* e = w.sh + ((size_t)li * w.n + p) * 2;
+                d               = e[0];
+                c               = e[1];
+            }
+            Ray r;
             r.o = mk(o.x, o.y, o.z);
             r.d = mk(d.x, d.y, d.z);
-            ++shadow;
-            if (!scene_any(sc, r, d.w, c.w, st)) L = cadd(L, mkc(c.x, c.y, c.z));
+            bool occ;
+            if (sc.packet) {
+                occ = scene_any_w(sc, r, d.w, c.w, on, w.diag ? &steps : nullptr);
+            } else {
+                occ = on ? scene_any(sc, r, d.w, c.w, st) : true;
+            }
+            if (on) {
+                ++shadow;
+                if (!occ) L = cadd(L, mkc(c.x, c.y, c.z));
+            }
         }
-        w.acc[p]           = w.acc[p] + L.r;
-        w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
-        w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
+        if (live) {
+            w.acc[p]           = w.acc[p] + L.r;
+            w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
+            w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
+        }
     }
-    wave_count(w.counters + 0, shadow); // occluded() counts the query as a ray too
-    wave_count(w.counters + 1, shadow);
+    if (w.diag)
+        diag_record(w.diag + ((size_t)(w.n >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * 4, t0, steps,
+                    (uint32_t)__popcll(__ballot(shadow != 0)));
+    unsigned long long* slot = w.wstat + ((size_t)(w.n >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * ST_N;
+    wave_count(slot, ST_RAYS, shadow); // occluded() counts the query as a ray too
+    wave_count(slot, ST_SHADOW, shadow);
 }
 
 __global__ void __launch_bounds__(WF_BLOCK) wf_resolve(Scene sc, WaveArgs w, float* out)
@@ -240,14 +314,44 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_resolve(Scene sc, WaveArgs w, flo
     o[0]     = a.r;
     o[1]     = a.g;
     o[2]     = a.b;
-    wave_count(w.counters + 2, pr.inside ? w.spp : 0u);
+    wave_count(w.wstat + (size_t)(p >> 6) * ST_N, ST_SAMPLES, pr.inside ? w.spp : 0u);
+}
+
+// Frame statistics: sum the per-wave slots (a few hundred atomics per frame).
+__global__ void __launch_bounds__(WF_BLOCK) wf_stats(WaveArgs w, int64_t n_slots)
+{
+    __shared__ unsigned long long part[ST_N][WF_BLOCK / 64];
+    unsigned long long v[ST_N] = {};
+    for (int64_t i = (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x; i < n_slots; i += (int64_t)gridDim.x * WF_BLOCK)
+        for (int k = 0; k < ST_N; ++k) v[k] += w.wstat[i * ST_N + k];
+    for (int k = 0; k < ST_N; ++k) {
+        unsigned long long x = v[k];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+        if ((threadIdx.x & 63) == 0) part[k][threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < ST_N) {
+        unsigned long long x = 0;
+        for (int j = 0; j < WF_BLOCK / 64; ++j) x += part[threadIdx.x][j];
+        const int map[ST_N] = { 0, 1, 2, 3, 4 }; // counters: rays, shadow, samples, draws, hits
+        if (x) atomicAdd(w.counters + map[threadIdx.x], x);
+    }
 }
 
 // ---------------------------------------------------------------------------- host side
+static uint32_t diag_sample_env()
+{
+    const char* v = std::getenv("SP_WAVE_DIAG_SAMPLE");
+    return v ? (uint32_t)std::atoi(v) : 0u;
+}
+
 size_t wave_bytes_per_pixel(int n_lights)
 {
     return 3 * 4 + 4 + 16 + 16 + (size_t)n_lights * 32 + 4 + 2 * MT_N * 8;
 }
+// primary/shade/resolve slots (one per tile) + persistent shadow-wave slots (at most as many)
+size_t wave_stat_bytes(int64_t n) { return (size_t)2 * (size_t)(n >> 6) * ST_N * 8; }
+size_t wave_queue_bytes(int64_t n) { return (QSEG * qseg_cap(n) + QSEG * QSTRIDE) * 4; }
 
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
                        hipStream_t stream, hipEvent_t* ev)
@@ -257,29 +361,36 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         if (ev) (void)hipEventRecord(ev[e++], stream);
     };
     const unsigned grid      = (unsigned)((w.n + WF_BLOCK - 1) / WF_BLOCK);
-    const size_t   stack_lds = (size_t)(WF_BLOCK / 64) * sc.stack_depth * 64 * 4;
+    const size_t   stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_depth * 64 * 4;
     const size_t   rs_lds    = (size_t)(2 << sc.rsqrt_bits) * 4;
     // the shadow queue never exceeds n: a persistent grid sized to fill the chip
     const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)n_cu * traverse_blocks_per_cu));
     mark();
+    (void)hipMemsetAsync(w.wstat, 0, wave_stat_bytes(w.n), stream);
     hipLaunchKernelGGL(wf_init, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w);
     mark();
+    WaveArgs wd = w; // diagnostics: only the launches of sample diag_sample record
+    wd.diag     = nullptr;
+    const uint32_t diag_sample = diag_sample_env();
     for (uint32_t i = 0; i < w.spp; ++i) {
-        hipLaunchKernelGGL(wf_primary, dim3(grid), dim3(WF_BLOCK), stack_lds, stream, sc, w, i);
+        const WaveArgs& wi = (w.diag && i == diag_sample) ? w : wd;
+        hipLaunchKernelGGL(wf_primary, dim3(grid), dim3(WF_BLOCK), stack_lds, stream, sc, wi, i);
         mark();
         hipLaunchKernelGGL(wf_shade, dim3(grid), dim3(WF_BLOCK), rs_lds, stream, sc, w, i);
         mark();
-        hipLaunchKernelGGL(wf_shadow, dim3(sgrid), dim3(WF_BLOCK), stack_lds, stream, sc, w);
+        hipLaunchKernelGGL(wf_shadow, dim3(sgrid), dim3(WF_BLOCK), stack_lds, stream, sc, wi);
         mark();
     }
     hipLaunchKernelGGL(wf_resolve, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w, out);
+    const int64_t n_slots = (w.n >> 6) + (int64_t)sgrid * (WF_BLOCK / 64);
+    hipLaunchKernelGGL(wf_stats, dim3(64), dim3(WF_BLOCK), 0, stream, w, n_slots);
     mark();
     return hipGetLastError();
 }
 
 int wave_traverse_blocks_per_cu(const Scene& sc)
 {
-    const size_t stack_lds = (size_t)(WF_BLOCK / 64) * sc.stack_depth * 64 * 4;
+    const size_t stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_depth * 64 * 4;
     int          n         = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shadow, WF_BLOCK, stack_lds) != hipSuccess) return 1;
     return n > 0 ? n : 1;

@@ -16,15 +16,19 @@ struct WaveArgs {
     float4*             hit;       // [n]
     float4*             shp;       // [n]
     float4*             sh;        // [n_lights][n][2]
-    uint32_t*           queue;     // [n]
-    uint32_t*           qcount;
+    uint32_t*           queue;     // QSEG segments (sp_wave.hip) of shadow-ray pixel slots
+    uint32_t*           qcount;    // QSEG segment counters, QSTRIDE words apart
     uint64_t*           mt_state;  // [n/64][2][312][64]
     unsigned long long* counters;  // [rays, shadow_rays, samples, draws, primary_hits]
+    unsigned long long* wstat;     // per-wave statistics slots (wave_stat_bytes)
+    unsigned long long* diag;      // optional per-wave timeline (SP_WAVE_DIAG): 4 u64 per wave
 };
 
 constexpr int WF_MAX_LIGHTS = 32; // light mask is one u32 per pixel
 
 size_t     wave_bytes_per_pixel(int n_lights);
+size_t     wave_stat_bytes(int64_t n);
+size_t     wave_queue_bytes(int64_t n);
 // ev: optional 3 * spp + 3 events recorded around every launch (stage timing)
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
                        hipStream_t stream, hipEvent_t* ev);

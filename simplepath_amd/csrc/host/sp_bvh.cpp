@@ -7,6 +7,8 @@
 // SAH (Wald 2007) with the same node format; it changes only the visiting order.
 #include "sp_host.hpp"
 
+#include <stdexcept>
+
 #include <algorithm>
 #include <cmath>
 #include <functional>
@@ -206,7 +208,7 @@ struct SahBuilder {
         const uint32_t r = build(mid, last, depth + 1);
         BvhNode& nd = nodes[me];
         for (int i = 0; i < 3; ++i) { nd.lo[i] = bb.lo[i]; nd.hi[i] = bb.hi[i]; }
-        nd.a = l;
+        nd.a = l | (static_cast<uint32_t>(best_dim) << BVH_AXIS_SHIFT); // split axis: near-first order
         nd.b = r;
         return me;
     }
@@ -226,6 +228,7 @@ Bvh build_bvh_sah(const std::vector<PrimBounds>& bounds, int max_leaf)
         b.cy[i]  = center_of(bounds[i], 1);
         b.cz[i]  = center_of(bounds[i], 2);
     }
+    if (n >= (size_t(1) << BVH_AXIS_SHIFT)) throw std::runtime_error("too many primitives for the SAH BVH");
     if (n) b.build(0, n, 1);
     out.nodes      = std::move(b.nodes);
     out.prim_order = std::move(b.ids);

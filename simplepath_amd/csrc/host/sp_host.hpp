@@ -106,6 +106,10 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 32, "BvhNode layout");
 constexpr uint32_t BVH_LEAF = 0x80000000u;
+// SAH builds store the split axis of an internal node in the top bits of `a` (0..2); the
+// reference-order build leaves them 0.  Child index = a & BVH_CHILD_MASK.
+constexpr uint32_t BVH_AXIS_SHIFT = 30;
+constexpr uint32_t BVH_CHILD_MASK = (1u << BVH_AXIS_SHIFT) - 1u;
 
 struct Bvh {
     std::vector<BvhNode> nodes;

@@ -100,7 +100,7 @@ def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
     assert np.array_equal(m.view(np.uint32), w.view(np.uint32)), rel_l2(w, m)
     assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
         (wst.rays, wst.shadow_rays, wst.samples, wst.rng_draws)
-    assert wst.launches == 2 + 3 * 5 and mst.launches == 1
+    assert wst.launches == 3 + 3 * 5 and mst.launches == 1
 
 
 def test_wavefront_tile_chunks(scene_dir, monkeypatch):
@@ -111,7 +111,7 @@ def test_wavefront_tile_chunks(scene_dir, monkeypatch):
     monkeypatch.setenv("SP_WAVE_MAX_GB", "0.0016")  # ~5 tiles per chunk
     a, ast = sp.render_tiles(s, "direct_lighting", 3, ids, pipeline="wavefront")
     b, _ = sp.render_tiles(s, "direct_lighting", 3, None, pipeline="wavefront")
-    assert ast.launches > 2 + 3 * 3
+    assert ast.launches > 3 + 3 * 3
     assert np.array_equal(a, ref)
     assert np.array_equal(b[ids], ref)
 
