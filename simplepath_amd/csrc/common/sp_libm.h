@@ -22,6 +22,35 @@ namespace spm {
 
 SP_HD double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 SP_HD double gd(const uint64_t* t, int i) { return u2d(t[i]); }
+
+// Tables read with a per-lane index.  In device code they are served from LDS copies (a
+// 64-lane gather from a global table touches several cache lines per instruction and keeps the
+// vector L1 busy); every kernel that can reach this libm calls libm_lds_init() first.
+#if defined(__HIP_DEVICE_COMPILE__)
+static __shared__ uint64_t lds_exp2f_t[32];
+static __shared__ uint64_t lds_logf_t[32];
+static __shared__ uint64_t lds_powf_t[32];
+static __shared__ uint64_t lds_sincosf_t[28];
+__device__ __forceinline__ void libm_lds_init(int tid, int nthreads)
+{
+    for (int i = tid; i < 32; i += nthreads) {
+        lds_exp2f_t[i] = glibc::EXP2F_T[i];
+        lds_logf_t[i]  = glibc::LOGF_T[i];
+        lds_powf_t[i]  = glibc::POWF_T[i];
+        if (i < 28) lds_sincosf_t[i] = glibc::SINCOSF_T[i];
+    }
+}
+#define SPM_EXP2F_T lds_exp2f_t
+#define SPM_LOGF_T lds_logf_t
+#define SPM_POWF_T lds_powf_t
+#define SPM_SINCOSF_T lds_sincosf_t
+#else
+SP_HD void libm_lds_init(int, int) {} // host pass / host build: tables are read in place
+#define SPM_EXP2F_T glibc::EXP2F_T
+#define SPM_LOGF_T glibc::LOGF_T
+#define SPM_POWF_T glibc::POWF_T
+#define SPM_SINCOSF_T glibc::SINCOSF_T
+#endif
 SP_HD float gf(const uint32_t* t, int i) { return u2f(t[i]); }
 
 // x86 default NaN produced by invalid operations such as 0/0 (sign bit set).
@@ -56,7 +85,7 @@ SP_HD float lm_expf(float x)
     const uint64_t ki    = d2u(kd);
     kd -= shift;
     const double r = dfma(invln2n, xd, -kd);
-    uint64_t     t = EXP2F_T[ki & 31u] + (ki << 47);
+    uint64_t     t = SPM_EXP2F_T[ki & 31u] + (ki << 47);
     const double s  = u2d(t);
     const double z  = dfma(r, gd(EXPF_K, 2), gd(EXPF_K, 3));
     const double r2 = r * r;
@@ -83,7 +112,7 @@ SP_HD float lm_logf(float x)
     const uint32_t i    = (tmp >> 19) & 15u;
     const int32_t  k    = (int32_t)tmp >> 23;
     const uint32_t iz   = ix - (tmp & 0xff800000u);
-    const double   invc = gd(LOGF_T, 2 * i), logc = gd(LOGF_T, 2 * i + 1);
+    const double   invc = gd(SPM_LOGF_T, 2 * i), logc = gd(SPM_LOGF_T, 2 * i + 1);
     const double   z    = (double)u2f(iz);
     const double   r    = dfma(z, invc, gd(MINUS_ONE_D, 0));
     const double   y0   = dfma((double)k, gd(LOGF_K, 0), logc);
@@ -144,7 +173,7 @@ SP_HD float lm_powf(float x, float y)
     const uint32_t top  = tmp & 0xff800000u;
     const uint32_t iz   = ix - top;
     const int32_t  k    = (int32_t)top >> 23;
-    const double   invc = gd(POWF_T, 2 * i), logc = gd(POWF_T, 2 * i + 1);
+    const double   invc = gd(SPM_POWF_T, 2 * i), logc = gd(SPM_POWF_T, 2 * i + 1);
     const double   z    = (double)u2f(iz);
     const double   r    = dfma(z, invc, gd(MINUS_ONE_D, 0));
     const double   y0   = (double)k + logc;
@@ -172,7 +201,7 @@ SP_HD float lm_powf(float x, float y)
     const uint64_t ki    = d2u(kd);
     kd -= shift;
     const double   rr  = ylogx - kd;
-    uint64_t       t   = EXP2F_T[ki & 31u];
+    uint64_t       t   = SPM_EXP2F_T[ki & 31u];
     const uint64_t ski = ki + sign_bias;
     t += ski << 47;
     const double s   = u2d(t);
@@ -186,7 +215,7 @@ SP_HD float lm_powf(float x, float y)
 
 // ------------------------------------------------------------------------------------ sinf / cosf
 // __sincosf_table[2] layout (14 doubles each): sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4
-SP_HD double sc(int tab, int k) { return gd(glibc::SINCOSF_T, tab * 14 + k); }
+SP_HD double sc(int tab, int k) { return gd(SPM_SINCOSF_T, tab * 14 + k); }
 enum { SC_HPI_INV = 4, SC_HPI = 5, SC_C0 = 6, SC_C1 = 7, SC_S1 = 8, SC_C2 = 9, SC_S2 = 10, SC_C3 = 11, SC_S3 = 12, SC_C4 = 13 };
 
 SP_HD float sincosf_poly(double x, double x2, int tab, int n)

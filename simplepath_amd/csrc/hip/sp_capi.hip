@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -50,6 +51,56 @@ sph::PrimBounds tri_bounds(const sph::Scene& s, int t)
         }
     }
     return b;
+}
+
+// Pair-node copy of a binary BVH: pair k = the two children of the k-th internal node (DFS
+// preorder), 16 floats {lo0, hi0, lo1, hi1, ref0, ref1, split axis, 0} (sp_path.hpp).
+std::vector<float4> pair_nodes(const sph::Bvh& bvh)
+{
+    const auto&           bn = bvh.nodes;
+    std::vector<uint32_t> pair_of(bn.size(), spd::PNONE);
+    uint32_t              np = 0;
+    std::vector<uint32_t> todo{ 0 };
+    while (!todo.empty()) { // preorder numbering of internal nodes
+        const uint32_t i = todo.back();
+        todo.pop_back();
+        if (bn[i].b & sph::BVH_LEAF) continue;
+        pair_of[i] = np++;
+        todo.push_back(bn[i].b);
+        todo.push_back(bn[i].a & sph::BVH_CHILD_MASK);
+    }
+    auto ref_of = [&](uint32_t i) -> uint32_t {
+        if (bn[i].b & sph::BVH_LEAF) {
+            const uint32_t cnt = bn[i].b & ~sph::BVH_LEAF;
+            if (cnt > 7 || bn[i].a > 0x0fffffffu) throw std::runtime_error("leaf does not fit a pair reference");
+            return spd::PLEAF | (cnt << 28) | bn[i].a;
+        }
+        return pair_of[i];
+    };
+    auto u2f = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
+    std::vector<float4> out;
+    if (bn[0].b & sph::BVH_LEAF) { // single leaf: one pair with an empty second child
+        const auto& r = bn[0];
+        out.push_back(make_float4(r.lo[0], r.lo[1], r.lo[2], r.hi[0]));
+        out.push_back(make_float4(r.hi[1], r.hi[2], 0.0f, 0.0f));
+        out.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        out.push_back(make_float4(u2f(ref_of(0)), u2f(spd::PNONE), u2f(0), 0.0f));
+        return out;
+    }
+    out.resize((size_t)np * 4);
+    for (size_t i = 0; i < bn.size(); ++i) {
+        if (pair_of[i] == spd::PNONE) continue;
+        const auto&    n = bn[i];
+        const uint32_t l = n.a & sph::BVH_CHILD_MASK, r = n.b;
+        const auto&    L = bn[l];
+        const auto&    R = bn[r];
+        float4*        q = &out[(size_t)pair_of[i] * 4];
+        q[0] = make_float4(L.lo[0], L.lo[1], L.lo[2], L.hi[0]);
+        q[1] = make_float4(L.hi[1], L.hi[2], R.lo[0], R.lo[1]);
+        q[2] = make_float4(R.lo[2], R.hi[0], R.hi[1], R.hi[2]);
+        q[3] = make_float4(u2f(ref_of(l)), u2f(ref_of(r)), u2f(n.a >> sph::BVH_AXIS_SHIFT), 0.0f);
+    }
+    return out;
 }
 
 spm::aff from_desc(const sp_affine& d)
@@ -115,6 +166,9 @@ struct sp_scene {
     void*                wave_buf     = nullptr; // wavefront pipeline state (sp_wave.hpp WaveArgs)
     size_t               wave_cap     = 0;
     std::vector<hipEvent_t> stage_ev;            // SP_RENDER_STAGE_TIMING
+    hipStream_t          aux_stream   = nullptr; // second part of the wavefront pipeline
+    hipEvent_t           ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t           ev_shade[2] = { nullptr, nullptr };
     int                  n_cu         = 0;
     hipEvent_t           ev0 = nullptr, ev1 = nullptr;
 
@@ -132,6 +186,15 @@ struct sp_scene {
         wave_cap = 0;
         for (hipEvent_t e : stage_ev) (void)hipEventDestroy(e);
         stage_ev.clear();
+        if (aux_stream) (void)hipStreamDestroy(aux_stream);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        for (hipEvent_t& e : ev_shade) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
+        aux_stream = nullptr;
+        ev_fork = ev_join = nullptr;
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
@@ -407,10 +470,20 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
                 slot_tri[3 * sl + k] = make_float4(v.x, v.y, v.z, 0.0f);
             }
         }
+        // the primitive code rides in p0.w so a triangle test is three 16-byte fetches
+        uint32_t code = slot_code[sl];
+        std::memcpy(&slot_tri[3 * sl].w, &code, 4);
     }
     std::vector<spd::Node> nodes(bvh.nodes.size());
     static_assert(sizeof(spd::Node) == sizeof(sph::BvhNode), "node layout");
     std::memcpy(nodes.data(), bvh.nodes.data(), nodes.size() * sizeof(spd::Node));
+    std::vector<float4> pairs; // SAH: pair-node copy (sp_path.hpp pair_closest / pair_any)
+    if (bvh_mode != 1 && !nodes.empty()) {
+        // opt-in (SP_PAIRS=1): the bunny frame is bound by vector-L1 accesses, which pair nodes
+        // do not reduce (same bytes per box), and their t0 stack halves the LDS occupancy
+        const bool use_pairs = std::getenv("SP_PAIRS") && std::atoi(std::getenv("SP_PAIRS")) != 0;
+        if (use_pairs) pairs = pair_nodes(bvh);
+    }
 
     // ---- lights: Scene::m_lights order + accelerator (partition by boundedness)
     std::vector<spd::Light> lights;
@@ -451,6 +524,8 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     up(unbounded, &d.unbounded);
     d.n_nodes = (int)nodes.size();
     up(nodes, &d.nodes);
+    d.pairs = nullptr;
+    if (!pairs.empty()) up(pairs, &d.pairs);
     up(slot_tri, &d.slot_tri);
     up(slot_code, &d.slot_code);
     std::vector<float> nrm(h.normals.size() * 3);
@@ -477,9 +552,12 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     s->geom_nodes  = nodes.size();
     s->geom_slots  = slot_code.size();
     d.stack_depth  = std::max(bvh.max_depth, lbvh.max_depth) + 1;
-    d.packet       = d.stack_depth <= 64 ? 1 : 0; // sp_packet.hpp PACKET_MAX_DEPTH
+    d.stack_words  = d.stack_depth * (d.pairs ? 2 : 1);
+    // Wave-coherent traversal (sp_packet.hpp) is opt-in (SP_PACKET=1): on the bunny frame the
+    // per-lane walk is faster (profiles/r01: packet steps are one dependent fetch per wave).
+    d.packet       = 0;
     d.ordered      = bvh_mode == 1 ? 0 : 1;       // reference order is part of the bit-exact contract
-    if (const char* v = std::getenv("SP_PACKET")) d.packet = d.packet && std::atoi(v) != 0;
+    if (const char* v = std::getenv("SP_PACKET")) d.packet = (d.stack_depth <= 64) && std::atoi(v) != 0;
     if (const char* v = std::getenv("SP_ORDERED")) d.ordered = d.ordered && std::atoi(v) != 0;
     SP_HIP(hipMalloc(&s->tile_counter, sizeof(int32_t)));
     SP_HIP(hipMalloc(&s->counters, 8 * sizeof(unsigned long long)));
@@ -536,7 +614,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
     int launches = 0;
     if (pipeline == SP_PIPELINE_WAVEFRONT) {
-        const size_t stack_lds = (size_t)4 * s->dev.stack_depth * 64 * 4;
+        const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
         if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         // Pixels in flight per pass: all requested tiles unless the state would exceed the budget
         // (SP_WAVE_MAX_GB, default 64 GB of the 288 GB HBM); larger jobs run in tile chunks.
@@ -581,6 +659,15 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         }
         w.diag = d_diag;
         const int per_cu = spd::wave_traverse_blocks_per_cu(s->dev);
+        int       n_parts = 2;
+        if (const char* v = std::getenv("SP_WAVE_PARTS")) n_parts = std::atoi(v);
+        if (n_parts > 1 && !s->aux_stream) {
+            SP_HIP(hipStreamCreateWithFlags(&s->aux_stream, hipStreamNonBlocking));
+            SP_HIP(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+            SP_HIP(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+            SP_HIP(hipEventCreateWithFlags(&s->ev_shade[0], hipEventDisableTiming));
+            SP_HIP(hipEventCreateWithFlags(&s->ev_shade[1], hipEventDisableTiming));
+        }
         const size_t n_ev = timing ? 3 * (size_t)w.spp + 3 : 0;
         while (s->stage_ev.size() < n_ev) {
             hipEvent_t e;
@@ -606,8 +693,11 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
                 SP_HIP(hipStreamSynchronize(stream));
                 w.tile_ids = s->d_tiles;
             }
+            w.pb = 0;
+            w.pe = w.n;
             SP_HIP(spd::wave_render(s->dev, w, d_out + (size_t)t0 * 64 * 3, per_cu, s->n_cu, stream,
-                                    timing ? s->stage_ev.data() : nullptr));
+                                    timing ? s->stage_ev.data() : nullptr, n_parts > 1 ? s->aux_stream : nullptr,
+                                    s->ev_fork, s->ev_join, s->ev_shade));
             launches += 3 + 3 * (int)w.spp;
             if (d_diag) {
                 std::vector<unsigned long long> h(diag_n);
@@ -639,7 +729,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         }
     } else {
         const int    rs_words  = 2 << s->dev.rsqrt_bits;
-        const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_depth * 64 * 4;
+        const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         int variant = 0;
         if (const char* v = std::getenv("SP_KERNEL_VARIANT")) variant = std::atoi(v);

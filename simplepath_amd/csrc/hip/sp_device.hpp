@@ -25,6 +25,8 @@ constexpr uint32_t CODE_SHIFT = 30;
 constexpr uint32_t CODE_MASK  = (1u << CODE_SHIFT) - 1u;
 constexpr uint32_t AXIS_SHIFT = 30;                      // sp_host.hpp BVH_AXIS_SHIFT
 constexpr uint32_t CHILD_MASK = (1u << AXIS_SHIFT) - 1u;
+constexpr uint32_t PLEAF      = 0x80000000u; // pair-node child reference: leaf flag
+constexpr uint32_t PNONE      = 0xffffffffu; // pair-node child reference: no child
 
 struct Node {
     float    lo[3];
@@ -66,6 +68,7 @@ struct Scene {
     const int32_t*  unbounded; // shape indices (planes), reference partition order
     int             n_nodes;
     const Node*     nodes;
+    const float4*   pairs;     // pair-node copy of an SAH BVH (sp_path.hpp), nullptr otherwise
     const float4*   slot_tri;  // 3 per slot
     const uint32_t* slot_code;
     const float*    normals;   // 3 per vertex
@@ -88,6 +91,7 @@ struct Scene {
     int32_t         rsqrt_bits;
     uint32_t        rsqrt_zero, rsqrt_denorm;
     int             stack_depth;   // LDS traversal stack entries per lane
+    int             stack_words;   // LDS words per lane (2 per entry for the pair-node walk)
     int             packet;        // 1: BVHs shallow enough for the wave-coherent walk (sp_packet.hpp)
     int             ordered;       // 1: SAH BVH -- visit the near child (split axis, ray sign) first
 };

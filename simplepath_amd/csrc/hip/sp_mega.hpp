@@ -33,9 +33,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
     const int wave = tid >> 6;
     const int rs_words = 2 << sc.rsqrt_bits;
     for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
+    libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
     __syncthreads();
     Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
-    Stack st{ lds + rs_words + wave * sc.stack_depth * 64, lane };
+    Stack st{ lds + rs_words + wave * sc.stack_words * 64, lane, sc.stack_depth };
 
     const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;
     Rng          rng;

@@ -268,10 +268,11 @@ __device__ __forceinline__ Isect finish_hit(const Scene& sc, const Hit& h, const
 // Test one primitive code against the ray (closest-hit semantics: t <= tmax accepted).
 __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h)
 {
-    const uint32_t code = sc.slot_code[slot];
+    const float4   q0   = sc.slot_tri[3 * slot]; // p0 | code
+    const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     if (kind == KIND_TRI) {
-        const float4 q0 = sc.slot_tri[3 * slot], q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
+        const float4 q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
         float t, be, ga;
         if (tri_hit(q0, q1, q2, ray, tmin, h.t, t, be, ga)) {
             h.t = t; h.code = code; h.beta = be; h.gamma = ga;
@@ -288,10 +289,11 @@ __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, con
 
 __device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, float tmax)
 {
-    const uint32_t code = sc.slot_code[slot];
+    const float4   q0   = sc.slot_tri[3 * slot]; // p0 | code
+    const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     if (kind == KIND_TRI) {
-        const float4 q0 = sc.slot_tri[3 * slot], q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
+        const float4 q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
         float t, be, ga;
         return tri_hit(q0, q1, q2, ray, tmin, tmax, t, be, ga);
     }
@@ -306,6 +308,7 @@ __device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const R
 struct Stack {
     uint32_t* s;
     int       lane;
+    int       depth; // entries; pair traversal keeps each entry's entry distance at s[(e + depth) * 64 + lane]
 };
 
 // SAH nodes carry their split axis: the child on the far side of the ray's direction goes on
@@ -316,6 +319,134 @@ __device__ __forceinline__ bool near_is_second(uint32_t a, const f3& d)
     const uint32_t ax = a >> AXIS_SHIFT;
     const float    da = (ax == 0) ? d.x : ((ax == 1) ? d.y : d.z);
     return da < 0.0f;
+}
+
+
+// ------------------------------------------------------------------------------ pair-node BVH
+// SAH builds are also stored as "pair nodes" (16 floats): the boxes of BOTH children of an
+// internal binary node plus their references, so one 64-byte fetch tests two boxes and a culled
+// child costs no fetch at all.  ref: internal = pair index; leaf = PLEAF | count << 28 | first
+// slot; PNONE = no child (single-leaf tree).  The closest-hit walk keeps each deferred child's
+// entry distance t0 on the stack and drops it on pop when t0 > current t_max -- exactly the box
+// test the deferred child would fail at that time (t_min unchanged, t_max only shrinks).
+
+__device__ __forceinline__ bool pair_box(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r,
+                                         const f3& inv, float tmin, float tmax, float& t0_out)
+{
+    float t0 = tmin, t1 = tmax; // same operation order as box_hit (math/BBox.h:254)
+    {
+        float tn = (lx - r.o.x) * inv.x, tf = (hx - r.o.x) * inv.x;
+        if (tn > tf) { const float s = tn; tn = tf; tf = s; }
+        t0 = std_max(tn, t0);
+        t1 = std_min(tf, t1);
+        if (t0 > t1) return false;
+    }
+    {
+        float tn = (ly - r.o.y) * inv.y, tf = (hy - r.o.y) * inv.y;
+        if (tn > tf) { const float s = tn; tn = tf; tf = s; }
+        t0 = std_max(tn, t0);
+        t1 = std_min(tf, t1);
+        if (t0 > t1) return false;
+    }
+    {
+        float tn = (lz - r.o.z) * inv.z, tf = (hz - r.o.z) * inv.z;
+        if (tn > tf) { const float s = tn; tn = tf; tf = s; }
+        t0 = std_max(tn, t0);
+        t1 = std_min(tf, t1);
+        if (t0 > t1) return false;
+    }
+    t0_out = t0;
+    return true;
+}
+
+struct PairHits {
+    uint32_t near_ref, far_ref;
+    float    far_t0;
+    int      n; // 0, 1 (near_ref) or 2 (near_ref first, far_ref deferred)
+};
+__device__ __forceinline__ PairHits pair_visit(const Scene& sc, uint32_t ref, const Ray& ray, const f3& inv, float tmin,
+                                               float tmax)
+{
+    const float4* q  = sc.pairs + 4 * (size_t)ref;
+    const float4  a  = q[0], b = q[1], c = q[2], d = q[3];
+    const uint32_t r0 = __float_as_uint(d.x), r1 = __float_as_uint(d.y), ax = __float_as_uint(d.z);
+    float         t0a = 0.0f, t0b = 0.0f;
+    const bool    ha = r0 != PNONE && pair_box(a.x, a.y, a.z, a.w, b.x, b.y, ray, inv, tmin, tmax, t0a);
+    const bool    hb = r1 != PNONE && pair_box(b.z, b.w, c.x, c.y, c.z, c.w, ray, inv, tmin, tmax, t0b);
+    PairHits      h;
+    h.n        = (int)ha + (int)hb;
+    h.near_ref = ha ? r0 : r1;
+    h.far_ref  = r1;
+    h.far_t0   = t0b;
+    if (ha && hb && near_is_second(ax << AXIS_SHIFT, ray.d)) {
+        h.near_ref = r1;
+        h.far_ref  = r0;
+        h.far_t0   = t0a;
+    }
+    return h;
+}
+
+__device__ __forceinline__ void pair_closest(const Scene& sc, const Ray& ray, float tmin, Hit& h, Stack st)
+{
+    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp  = 0;
+    uint32_t ref = 0;
+    while (true) {
+        if (!(ref & PLEAF)) {
+            const PairHits ph = pair_visit(sc, ref, ray, inv, tmin, h.t);
+            if (ph.n == 2) {
+                st.s[sp * 64 + st.lane]              = ph.far_ref;
+                st.s[(sp + st.depth) * 64 + st.lane] = __float_as_uint(ph.far_t0);
+                ++sp;
+            }
+            if (ph.n > 0) {
+                ref = ph.near_ref;
+                continue;
+            }
+        } else {
+            const uint32_t first = ref & 0x0fffffffu, cnt = (ref >> 28) & 7u;
+            for (uint32_t k = 0; k < cnt; ++k) prim_closest(sc, first + k, ray, tmin, h);
+        }
+        bool more = false;
+        while (sp > 0) {
+            --sp;
+            const float t0 = __uint_as_float(st.s[(sp + st.depth) * 64 + st.lane]);
+            if (!(t0 > h.t)) {
+                ref  = st.s[sp * 64 + st.lane];
+                more = true;
+                break;
+            }
+        }
+        if (!more) break;
+    }
+}
+
+__device__ __forceinline__ bool pair_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp  = 0;
+    uint32_t ref = 0;
+    while (true) {
+        if (!(ref & PLEAF)) {
+            const PairHits ph = pair_visit(sc, ref, ray, inv, tmin, tmax);
+            if (ph.n == 2) {
+                st.s[sp * 64 + st.lane] = ph.far_ref;
+                ++sp;
+            }
+            if (ph.n > 0) {
+                ref = ph.near_ref;
+                continue;
+            }
+        } else {
+            const uint32_t first = ref & 0x0fffffffu, cnt = (ref >> 28) & 7u;
+            for (uint32_t k = 0; k < cnt; ++k)
+                if (prim_any(sc, first + k, ray, tmin, tmax)) return true;
+        }
+        if (sp == 0) break;
+        --sp;
+        ref = st.s[sp * 64 + st.lane];
+    }
+    return false;
 }
 
 // Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
@@ -332,6 +463,10 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
         if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
     if (sc.n_nodes == 0) return h;
+    if (sc.pairs) {
+        pair_closest(sc, ray, tmin, h, st);
+        return h;
+    }
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     int      sp  = 0;
     uint32_t cur = 0;      // root: no box test
@@ -369,6 +504,7 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
         if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
     }
     if (sc.n_nodes == 0) return false;
+    if (sc.pairs) return pair_any(sc, ray, tmin, tmax, st);
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     int      sp  = 0;
     uint32_t cur = 0;

@@ -114,8 +114,8 @@ __device__ __forceinline__ void rng_store(const WaveArgs& w, int64_t p, const Rn
 
 __global__ void __launch_bounds__(WF_BLOCK) wf_init(Scene sc, WaveArgs w)
 {
-    const int64_t p = (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
-    if (p >= w.n) return;
+    const int64_t p = w.pb + (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
+    if (p >= w.pe) return;
     const PixelRef pr = pixel_of(sc, w, p);
     w.acc[p] = 0.0f;
     w.acc[w.n + p] = 0.0f;
@@ -134,10 +134,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_init(Scene sc, WaveArgs w)
 __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uint32_t sample)
 {
     extern __shared__ uint32_t lds[];
-    const int64_t p    = (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
+    const int64_t p    = w.pb + (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
     const int     lane = threadIdx.x & 63;
     if (blockIdx.x == 0 && threadIdx.x < QSEG) w.qcount[threadIdx.x * QSTRIDE] = 0u; // previous wf_shadow is done
-    if (p >= w.n) return;
+    if (p >= w.pe) return;
     const uint64_t t0 = w.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t       steps = 0;
     const PixelRef pr = pixel_of(sc, w, p);
@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uin
             if (lh.hit) tmax = lh.t;
             h = scene_intersect_w(sc, ray, k_ray_epsilon, tmax, on, w.diag ? &steps : nullptr);
         } else {
-            const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_depth * 64, lane };
+            const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
             lh = scene_intersect_lights(sc, ray, k_ray_epsilon, tmax, st);
             if (lh.hit) tmax = lh.t;
             h = scene_intersect(sc, ray, k_ray_epsilon, tmax, st);
@@ -181,14 +181,15 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uin
 }
 
 // Shading: direct_nee's sampling half (Integrator.cpp:287-296).
-__global__ void __launch_bounds__(WF_BLOCK) wf_shade(Scene sc, WaveArgs w, uint32_t sample)
+__global__ void __launch_bounds__(WF_BLOCK, 3) wf_shade(Scene sc, WaveArgs w, uint32_t sample)
 {
     extern __shared__ uint32_t lds[];
     const int rs_words = 2 << sc.rsqrt_bits;
     for (int i = threadIdx.x; i < rs_words; i += WF_BLOCK) lds[i] = sc.rsqrt_entries[i];
+    libm_lds_init(threadIdx.x, WF_BLOCK);
     __syncthreads();
-    const int64_t p = (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
-    if (p >= w.n) return;
+    const int64_t p = w.pb + (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
+    if (p >= w.pe) return;
     const PixelRef pr = pixel_of(sc, w, p);
     uint32_t       mask = 0, draws = 0;
     if (pr.inside) {
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shade(Scene sc, WaveArgs w, uint3
         if (lane == 0) base = atomicAdd(w.qcount + seg * QSTRIDE, total);
         base = __shfl(base, 0, 64);
         if (mask)
-            w.queue[(size_t)seg * qseg_cap(w.n) + base + (uint32_t)__popcll(ballot & ((1ull << lane) - 1ull))] = (uint32_t)p;
+            w.queue[(size_t)seg * w.qcap + base + (uint32_t)__popcll(ballot & ((1ull << lane) - 1ull))] = (uint32_t)p;
     }
     wave_count(w.wstat + (size_t)(p >> 6) * ST_N, ST_DRAWS, draws);
 }
@@ -244,7 +245,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shadow(Scene sc, WaveArgs w)
 {
     extern __shared__ uint32_t lds[];
     const int      lane  = threadIdx.x & 63;
-    const Stack    st{ lds + (threadIdx.x >> 6) * sc.stack_depth * 64, lane };
+    const Stack    st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
     // Segment j holds the shadow pixels of tile slots j, j + QSEG, ... in arrival order.  Virtual
     // chunk v = 64 entries of segment v % QSEG starting at (v / QSEG) * 64: walking v in order
     // visits the tiles roughly in image order, which keeps neighbouring waves' BVH nodes in cache.
@@ -252,7 +253,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shadow(Scene sc, WaveArgs w)
     uint32_t       maxn   = segn;
     for (int off = 32; off > 0; off >>= 1) maxn = max(maxn, (uint32_t)__shfl_xor(maxn, off, 64));
     const uint32_t n_virt = QSEG * ((maxn + 63) / 64);
-    const size_t   cap    = qseg_cap(w.n);
+    const size_t   cap    = w.qcap;
     uint32_t       shadow = 0;
     const uint64_t t0     = w.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t       steps  = 0;
@@ -296,17 +297,17 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shadow(Scene sc, WaveArgs w)
         }
     }
     if (w.diag)
-        diag_record(w.diag + ((size_t)(w.n >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * 4, t0, steps,
+        diag_record(w.diag + ((size_t)(w.n >> 6) + (w.pb >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * 4, t0, steps,
                     (uint32_t)__popcll(__ballot(shadow != 0)));
-    unsigned long long* slot = w.wstat + ((size_t)(w.n >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * ST_N;
+    unsigned long long* slot = w.wstat + ((size_t)(w.n >> 6) + (w.pb >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * ST_N;
     wave_count(slot, ST_RAYS, shadow); // occluded() counts the query as a ray too
     wave_count(slot, ST_SHADOW, shadow);
 }
 
 __global__ void __launch_bounds__(WF_BLOCK) wf_resolve(Scene sc, WaveArgs w, float* out)
 {
-    const int64_t p = (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
-    if (p >= w.n) return;
+    const int64_t p = w.pb + (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
+    if (p >= w.pe) return;
     const PixelRef pr = pixel_of(sc, w, p);
     rgb            a  = mkc(w.acc[p], w.acc[w.n + p], w.acc[2 * w.n + p]);
     if (pr.inside) a = cdivs(a, (float)w.spp); // image(p) /= num_pixel_samples (main.cpp:102)
@@ -351,38 +352,82 @@ size_t wave_bytes_per_pixel(int n_lights)
 }
 // primary/shade/resolve slots (one per tile) + persistent shadow-wave slots (at most as many)
 size_t wave_stat_bytes(int64_t n) { return (size_t)2 * (size_t)(n >> 6) * ST_N * 8; }
-size_t wave_queue_bytes(int64_t n) { return (QSEG * qseg_cap(n) + QSEG * QSTRIDE) * 4; }
+// room for up to two parts (wave_render), each QSEG segments + QSEG counters
+size_t wave_queue_bytes(int64_t n) { return 2 * (QSEG * (qseg_cap(n) + 64) + QSEG * QSTRIDE) * 4; }
 
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
-                       hipStream_t stream, hipEvent_t* ev)
+                       hipStream_t stream, hipEvent_t* ev, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
+                       hipEvent_t* shade_done)
 {
     int  e    = 0;
     auto mark = [&]() {
         if (ev) (void)hipEventRecord(ev[e++], stream);
     };
-    const unsigned grid      = (unsigned)((w.n + WF_BLOCK - 1) / WF_BLOCK);
-    const size_t   stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_depth * 64 * 4;
-    const size_t   rs_lds    = (size_t)(2 << sc.rsqrt_bits) * 4;
-    // the shadow queue never exceeds n: a persistent grid sized to fill the chip
-    const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)n_cu * traverse_blocks_per_cu));
+    const size_t stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
+    const size_t rs_lds    = (size_t)(2 << sc.rsqrt_bits) * 4;
+    const unsigned grid_all = (unsigned)((w.n + WF_BLOCK - 1) / WF_BLOCK);
+
+    // Parts: contiguous tile ranges with their own queue, each driven by its own stream, so that
+    // one part's traversal kernels (memory-latency bound) overlap the other part's shading
+    // (VALU bound) on the same CUs.
+    const int   parts = (aux && w.n >= 2 * 64 * 256) ? 2 : 1;
+    WaveArgs    pw[2];
+    hipStream_t ps[2] = { stream, aux };
+    const int64_t slots = w.n >> 6;
+    int64_t       s0    = 0;
+    uint32_t*     q     = w.queue;
+    for (int k = 0; k < parts; ++k) {
+        const int64_t ns = (k == parts - 1) ? slots - s0 : slots / parts;
+        pw[k]            = w;
+        pw[k].pb         = s0 * 64;
+        pw[k].pe         = (s0 + ns) * 64;
+        pw[k].qcap       = qseg_cap(ns * 64);
+        pw[k].queue      = q;
+        pw[k].qcount     = q + QSEG * pw[k].qcap;
+        q += QSEG * pw[k].qcap + QSEG * QSTRIDE;
+        s0 += ns;
+    }
     mark();
     (void)hipMemsetAsync(w.wstat, 0, wave_stat_bytes(w.n), stream);
-    hipLaunchKernelGGL(wf_init, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w);
+    hipLaunchKernelGGL(wf_init, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, w);
     mark();
-    WaveArgs wd = w; // diagnostics: only the launches of sample diag_sample record
-    wd.diag     = nullptr;
-    const uint32_t diag_sample = diag_sample_env();
-    for (uint32_t i = 0; i < w.spp; ++i) {
-        const WaveArgs& wi = (w.diag && i == diag_sample) ? w : wd;
-        hipLaunchKernelGGL(wf_primary, dim3(grid), dim3(WF_BLOCK), stack_lds, stream, sc, wi, i);
-        mark();
-        hipLaunchKernelGGL(wf_shade, dim3(grid), dim3(WF_BLOCK), rs_lds, stream, sc, w, i);
-        mark();
-        hipLaunchKernelGGL(wf_shadow, dim3(sgrid), dim3(WF_BLOCK), stack_lds, stream, sc, wi);
-        mark();
+    if (parts > 1) {
+        (void)hipEventRecord(fork, stream);
+        (void)hipStreamWaitEvent(aux, fork, 0);
     }
-    hipLaunchKernelGGL(wf_resolve, dim3(grid), dim3(WF_BLOCK), 0, stream, sc, w, out);
-    const int64_t n_slots = (w.n >> 6) + (int64_t)sgrid * (WF_BLOCK / 64);
+    const uint32_t diag_sample = diag_sample_env();
+    unsigned       grid[2], sgrid[2];
+    WaveArgs       pd[2];
+    for (int k = 0; k < parts; ++k) {
+        grid[k]  = (unsigned)((pw[k].pe - pw[k].pb + WF_BLOCK - 1) / WF_BLOCK);
+        // the shadow queue never exceeds the part: a persistent grid sized to fill the chip
+        sgrid[k] = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid[k], (int64_t)n_cu * traverse_blocks_per_cu));
+        pd[k]      = pw[k]; // diagnostics: only the launches of sample diag_sample record
+        pd[k].diag = nullptr;
+    }
+    // With two parts the shading kernels alternate (A's shade, then B's, then A's ...) through a
+    // pair of cross-stream events, so each part's traversal kernels run beside the other part's
+    // shading instead of both parts shading at once.
+    for (uint32_t i = 0; i < w.spp; ++i) {
+        for (int k = 0; k < parts; ++k) {
+            const WaveArgs& wi = (pw[k].diag && i == diag_sample) ? pw[k] : pd[k];
+            hipStream_t     st = ps[k];
+            hipLaunchKernelGGL(wf_primary, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
+            if (k == 0) mark();
+            if (parts > 1 && (k == 1 || i > 0)) (void)hipStreamWaitEvent(st, shade_done[1 - k], 0);
+            hipLaunchKernelGGL(wf_shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, pd[k], i);
+            if (parts > 1) (void)hipEventRecord(shade_done[k], st);
+            if (k == 0) mark();
+            hipLaunchKernelGGL(wf_shadow, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
+            if (k == 0) mark();
+        }
+    }
+    if (parts > 1) {
+        (void)hipEventRecord(join, aux);
+        (void)hipStreamWaitEvent(stream, join, 0);
+    }
+    hipLaunchKernelGGL(wf_resolve, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, w, out);
+    const int64_t n_slots = 2 * slots;
     hipLaunchKernelGGL(wf_stats, dim3(64), dim3(WF_BLOCK), 0, stream, w, n_slots);
     mark();
     return hipGetLastError();
@@ -390,7 +435,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
 
 int wave_traverse_blocks_per_cu(const Scene& sc)
 {
-    const size_t stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_depth * 64 * 4;
+    const size_t stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
     int          n         = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shadow, WF_BLOCK, stack_lds) != hipSuccess) return 1;
     return n > 0 ? n : 1;

@@ -7,7 +7,8 @@
 namespace spd {
 
 struct WaveArgs {
-    int64_t             n;         // pixel slots in flight = tiles * 64
+    int64_t             n;         // pixel slots in flight = tiles * 64 (array strides)
+    int64_t             pb, pe;    // pixel slot range handled by this launch sequence
     const int32_t*      tile_ids;  // nullptr => identity
     int32_t             tiles_x;
     uint32_t            spp;
@@ -18,6 +19,7 @@ struct WaveArgs {
     float4*             sh;        // [n_lights][n][2]
     uint32_t*           queue;     // QSEG segments (sp_wave.hip) of shadow-ray pixel slots
     uint32_t*           qcount;    // QSEG segment counters, QSTRIDE words apart
+    size_t              qcap;      // entries per queue segment
     uint64_t*           mt_state;  // [n/64][2][312][64]
     unsigned long long* counters;  // [rays, shadow_rays, samples, draws, primary_hits]
     unsigned long long* wstat;     // per-wave statistics slots (wave_stat_bytes)
@@ -29,9 +31,11 @@ constexpr int WF_MAX_LIGHTS = 32; // light mask is one u32 per pixel
 size_t     wave_bytes_per_pixel(int n_lights);
 size_t     wave_stat_bytes(int64_t n);
 size_t     wave_queue_bytes(int64_t n);
-// ev: optional 3 * spp + 3 events recorded around every launch (stage timing)
+// ev: optional 3 * spp + 3 events recorded around the launches of part 0 (stage timing);
+// aux (may be null): second stream for the overlapped second part, fork/join its events.
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
-                       hipStream_t stream, hipEvent_t* ev);
+                       hipStream_t stream, hipEvent_t* ev, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
+                       hipEvent_t* shade_done /* [2] */);
 int        wave_traverse_blocks_per_cu(const Scene& sc);
 
 } // namespace spd
