@@ -201,6 +201,10 @@ def roofline_of(stats, pixels, args, kernel_ms):
     tot = [sum(s.stage_ms[k] for s in stats) / n for k in range(4)]
     spp = args.spp
     by = stage_bytes(st, pixels)
+    # stage events time part 0; with two parts it holds ceil(tiles / 2) of the interleaved tiles
+    tiles = (pixels + 63) // 64
+    frac0 = 0.5 if st.parts == 2 else 1.0  # blocks of tiles dealt alternately: about half
+    by = {k: v * frac0 for k, v in by.items()}
     stages = {}
     for k in (1, 2, 3):
         ms_launch = tot[k] / spp
@@ -214,6 +218,7 @@ def roofline_of(stats, pixels, args, kernel_ms):
     achieved = d["gbs"]
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": names[dom],
+            "parts": st.parts, "part0_fraction": round(frac0, 4),
             "kernel_ms": d["ms_per_launch"], "alg_bytes_per_launch": d["alg_bytes_per_launch"],
             "frame_kernel_ms": round(kernel_ms, 2), "stages": stages}
 

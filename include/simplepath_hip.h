@@ -185,7 +185,9 @@ typedef struct sp_render_stats {
     int32_t  launches;        /* kernel launches issued                                           */
     uint64_t primary_hits;    /* wavefront: camera rays that hit geometry (shading work items)     */
     float    stage_ms[4];     /* with SP_RENDER_STAGE_TIMING, wavefront: [init+resolve, primary,   */
-                              /* shade, shadow] summed over launches; megakernel: [0] = kernel     */
+                              /* shade, shadow] of part 0 summed over launches; megakernel: [0]   */
+    int32_t  parts;           /* wavefront: concurrent parts (streams); part 0 holds ceil(tiles/2) */
+    int32_t  reserved;
 } sp_render_stats;
 
 /* ---- API ------------------------------------------------------------------------------ */

@@ -48,6 +48,7 @@ class RenderStats:
     launches: int = 0
     primary_hits: int = 0
     stage_ms: tuple = (0.0, 0.0, 0.0, 0.0)
+    parts: int = 1
 
 
 class Scene:
@@ -176,7 +177,7 @@ def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeli
 
 def _stats(s: _abi.sp_render_stats) -> RenderStats:
     return RenderStats(s.rays, s.shadow_rays, s.samples, s.rng_draws, s.kernel_ms, s.pipeline, s.launches,
-                       s.primary_hits, tuple(s.stage_ms))
+                       s.primary_hits, tuple(s.stage_ms), s.parts)
 
 
 def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Optional[Sequence[int]] = None,

@@ -90,7 +90,8 @@ class sp_render_params(C.Structure):
 class sp_render_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
                 ("rng_draws", C.c_uint64), ("kernel_ms", C.c_float), ("pipeline", C.c_int32),
-                ("launches", C.c_int32), ("primary_hits", C.c_uint64), ("stage_ms", C.c_float * 4)]
+                ("launches", C.c_int32), ("primary_hits", C.c_uint64), ("stage_ms", C.c_float * 4),
+                ("parts", C.c_int32), ("reserved", C.c_int32)]
 
 
 # Every symbol declared in include/simplepath_hip.h, with its ctypes signature.

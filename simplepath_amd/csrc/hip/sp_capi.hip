@@ -612,7 +612,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         return fail(SP_ERR_UNSUPPORTED, "wavefront pipeline supports DirectLighting with <= 32 lights");
     if (pipeline == SP_PIPELINE_AUTO) pipeline = wave_ok ? SP_PIPELINE_WAVEFRONT : SP_PIPELINE_MEGAKERNEL;
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
-    int launches = 0;
+    int launches = 0, parts_used = 1;
     if (pipeline == SP_PIPELINE_WAVEFRONT) {
         const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
         if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
@@ -697,7 +697,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
             w.pe = w.n;
             SP_HIP(spd::wave_render(s->dev, w, d_out + (size_t)t0 * 64 * 3, per_cu, s->n_cu, stream,
                                     timing ? s->stage_ev.data() : nullptr, n_parts > 1 ? s->aux_stream : nullptr,
-                                    s->ev_fork, s->ev_join, s->ev_shade));
+                                    s->ev_fork, s->ev_join, s->ev_shade, &parts_used));
             launches += 3 + 3 * (int)w.spp;
             if (d_diag) {
                 std::vector<unsigned long long> h(diag_n);
@@ -774,6 +774,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         stats->pipeline    = pipeline;
         stats->launches    = launches;
         stats->primary_hits = c[4];
+        stats->parts        = parts_used;
         if (pipeline == SP_PIPELINE_MEGAKERNEL && timing) stage[0] = ms;
         for (int k = 0; k < 4; ++k) stats->stage_ms[k] = stage[k];
     }

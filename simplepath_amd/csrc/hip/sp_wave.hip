@@ -43,9 +43,25 @@ struct PixelRef {
     bool     inside;
 };
 
+// Internal slot -> caller's slot.  With two parts the caller's tiles are dealt in blocks of
+// ilv tiles, alternately (part 0 = blocks 0, 2, 4 ..., part 1 = blocks 1, 3, ...), so both parts
+// see a similar mix of cheap (sky) and expensive tiles while neighbouring tiles stay together.
+__host__ __device__ inline int64_t part0_slots(int64_t slots, int64_t ilv)
+{
+    const int64_t full = slots / ilv, rem = slots % ilv;
+    return ((full + 1) / 2) * ilv + ((full % 2 == 0) ? rem : 0);
+}
+__device__ __forceinline__ int64_t caller_slot(const WaveArgs& w, int64_t slot)
+{
+    if (!w.interleave) return slot;
+    const int64_t ilv = w.interleave, p0 = part0_slots(w.n >> 6, ilv);
+    const int64_t s   = slot < p0 ? slot : slot - p0;
+    return (2 * (s / ilv) + (slot < p0 ? 0 : 1)) * ilv + s % ilv;
+}
+
 __device__ __forceinline__ PixelRef pixel_of(const Scene& sc, const WaveArgs& w, int64_t p)
 {
-    const int64_t  slot = p >> 6;
+    const int64_t  slot = caller_slot(w, p >> 6);
     const uint32_t lane = (uint32_t)p & 63u;
     const int32_t  tile = w.tile_ids ? w.tile_ids[slot] : (int32_t)slot;
     PixelRef       r;
@@ -311,7 +327,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_resolve(Scene sc, WaveArgs w, flo
     const PixelRef pr = pixel_of(sc, w, p);
     rgb            a  = mkc(w.acc[p], w.acc[w.n + p], w.acc[2 * w.n + p]);
     if (pr.inside) a = cdivs(a, (float)w.spp); // image(p) /= num_pixel_samples (main.cpp:102)
-    float* o = out + (size_t)p * 3;
+    float* o = out + ((size_t)caller_slot(w, p >> 6) * 64 + (size_t)(p & 63)) * 3;
     o[0]     = a.r;
     o[1]     = a.g;
     o[2]     = a.b;
@@ -340,6 +356,12 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_stats(WaveArgs w, int64_t n_slots
 }
 
 // ---------------------------------------------------------------------------- host side
+static int32_t interleave_block_env()
+{
+    const char* v = std::getenv("SP_WAVE_ILV");
+    const int   b = v ? std::atoi(v) : 240; // one 1080p tile row (profiles/r01 sweep: 1..16200 within 3%)
+    return b > 0 ? b : 240;
+}
 static uint32_t diag_sample_env()
 {
     const char* v = std::getenv("SP_WAVE_DIAG_SAMPLE");
@@ -357,7 +379,7 @@ size_t wave_queue_bytes(int64_t n) { return 2 * (QSEG * (qseg_cap(n) + 64) + QSE
 
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
                        hipStream_t stream, hipEvent_t* ev, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
-                       hipEvent_t* shade_done)
+                       hipEvent_t* shade_done, int* parts_out)
 {
     int  e    = 0;
     auto mark = [&]() {
@@ -371,14 +393,17 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     // one part's traversal kernels (memory-latency bound) overlap the other part's shading
     // (VALU bound) on the same CUs.
     const int   parts = (aux && w.n >= 2 * 64 * 256) ? 2 : 1;
+    if (parts_out) *parts_out = parts;
     WaveArgs    pw[2];
     hipStream_t ps[2] = { stream, aux };
+    WaveArgs    wa    = w;
+    wa.interleave     = parts > 1 ? interleave_block_env() : 0;
     const int64_t slots = w.n >> 6;
     int64_t       s0    = 0;
     uint32_t*     q     = w.queue;
     for (int k = 0; k < parts; ++k) {
-        const int64_t ns = (k == parts - 1) ? slots - s0 : slots / parts;
-        pw[k]            = w;
+        const int64_t ns = (k == parts - 1) ? slots - s0 : part0_slots(slots, wa.interleave);
+        pw[k]            = wa;
         pw[k].pb         = s0 * 64;
         pw[k].pe         = (s0 + ns) * 64;
         pw[k].qcap       = qseg_cap(ns * 64);
@@ -389,7 +414,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     }
     mark();
     (void)hipMemsetAsync(w.wstat, 0, wave_stat_bytes(w.n), stream);
-    hipLaunchKernelGGL(wf_init, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, w);
+    hipLaunchKernelGGL(wf_init, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, wa);
     mark();
     if (parts > 1) {
         (void)hipEventRecord(fork, stream);
@@ -426,7 +451,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         (void)hipEventRecord(join, aux);
         (void)hipStreamWaitEvent(stream, join, 0);
     }
-    hipLaunchKernelGGL(wf_resolve, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, w, out);
+    hipLaunchKernelGGL(wf_resolve, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, wa, out);
     const int64_t n_slots = 2 * slots;
     hipLaunchKernelGGL(wf_stats, dim3(64), dim3(WF_BLOCK), 0, stream, w, n_slots);
     mark();

@@ -9,6 +9,7 @@ namespace spd {
 struct WaveArgs {
     int64_t             n;         // pixel slots in flight = tiles * 64 (array strides)
     int64_t             pb, pe;    // pixel slot range handled by this launch sequence
+    int32_t             interleave;// >0: tile block size dealt alternately to two parts (caller_slot)
     const int32_t*      tile_ids;  // nullptr => identity
     int32_t             tiles_x;
     uint32_t            spp;
@@ -35,7 +36,7 @@ size_t     wave_queue_bytes(int64_t n);
 // aux (may be null): second stream for the overlapped second part, fork/join its events.
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
                        hipStream_t stream, hipEvent_t* ev, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
-                       hipEvent_t* shade_done /* [2] */);
+                       hipEvent_t* shade_done /* [2] */, int* parts_out);
 int        wave_traverse_blocks_per_cu(const Scene& sc);
 
 } // namespace spd

@@ -103,6 +103,23 @@ def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
     assert wst.launches == 3 + 3 * 5 and mst.launches == 1
 
 
+def test_wavefront_two_parts(scene_dir, monkeypatch):
+    # >= 32768 pixels in flight: two interleaved parts on two streams (ragged: odd tile count)
+    s = load(scene_dir, "bunny.sp", 264, 128, bvh=0)
+    m, _ = sp.render_tiles(s, "direct_lighting", 2, pipeline="megakernel")
+    w, wst = sp.render_tiles(s, "direct_lighting", 2, pipeline="wavefront")
+    assert wst.parts == 2
+    assert np.array_equal(m.view(np.uint32), w.view(np.uint32)), rel_l2(w, m)
+    ids = np.arange(sp.TileScheduler(264, 128).get_num_tiles(), dtype=np.int32)[::-1].copy()
+    r, rst = sp.render_tiles(s, "direct_lighting", 2, ids, pipeline="wavefront")
+    assert rst.parts == 2
+    assert np.array_equal(r, w[ids])
+    monkeypatch.setenv("SP_WAVE_PARTS", "1")
+    one, ost = sp.render_tiles(s, "direct_lighting", 2, pipeline="wavefront")
+    assert ost.parts == 1
+    assert np.array_equal(one, w)
+
+
 def test_wavefront_tile_chunks(scene_dir, monkeypatch):
     # a tiny state budget forces several tile chunks per call; result must not change
     s = load(scene_dir, "bunny.sp", 64, 48, bvh=0)
