@@ -132,7 +132,7 @@ def main():
     cpu = None
     parity = None
     if not args.no_cpu:
-        cpu, parity = cpu_baseline(scene, integ, args, out if world == 1 else None, my_tiles)
+        cpu, parity = cpu_baseline(scene, path, integ, args, out if world == 1 else None, my_tiles)
 
     line = {
         "metric": "Mrays/sec (+ Msamples/sec) at fixed spp; per-pixel L2 vs CPU ref",
@@ -223,10 +223,31 @@ def roofline_of(stats, pixels, args, kernel_ms):
             "frame_kernel_ms": round(kernel_ms, 2), "stages": stages}
 
 
-def cpu_baseline(scene, integ, args, gpu_out, my_tiles):
-    """Time the CPU oracle (glibc = reference semantics, "port") on a bounded sample of the same
-    frame: whole 8x8 tiles spread over the image, same spp and integrator, until about
-    --cpu-seconds of work; also compares those tiles with the GPU frame (rel L2, bit-exact share)."""
+def _ref_lib():
+    """oracle/_ref/libsp_ref.so: the reference's own render path built from its sources (test
+    infrastructure, present when the reference was available at build time)."""
+    import ctypes as C
+    path = os.path.join(ROOT, "oracle", "_ref", "libsp_ref.so")
+    if not os.path.exists(path):
+        return None
+    L = C.CDLL(path)
+    L.ref_scene_create.restype = C.c_void_p
+    L.ref_scene_create.argtypes = [C.c_char_p, C.c_int, C.c_int]
+    L.ref_scene_free.argtypes = [C.c_void_p]
+    L.ref_render_tiles.restype = C.c_int
+    L.ref_render_tiles.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.POINTER(C.c_int32), C.c_int64, C.c_int,
+                                   C.POINTER(C.c_float)]
+    return L
+
+
+def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles):
+    """CPU baseline on a bounded sample of the same frame (whole 8x8 tiles spread over the image,
+    same spp and integrator, about --cpu-seconds of work): the reference itself (oracle/_ref,
+    kind "reference") when built, else the C oracle (kind "port").  Ray counts come from the
+    oracle on the same tiles (identical control flow: the two are bit-exact, tests/
+    test_oracle_vs_ref.py), which also checks the GPU frame on those tiles."""
+    import ctypes as C
+
     import simplepath_amd as sp
     from tests import _oracle
 
@@ -234,38 +255,55 @@ def cpu_baseline(scene, integ, args, gpu_out, my_tiles):
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     rng = np.random.default_rng(1234)
     order = rng.permutation(n_tiles).astype(np.int32)
-    done, t_used, rays, samples = [], 0.0, 0, 0
-    chunk = threads
-    tiles_out = []
+    ref = _ref_lib()
+    ref_scene = None
+    if ref is not None:  # parse + BVH build outside the timed region, as the reference's main does
+        ref_scene = ref.ref_scene_create(scene_path.encode(), args.width, args.height)
+        if not ref_scene:
+            ref = None
+    kind = "reference" if ref is not None else "port"
+
+    def run(ids):
+        if ref is not None:
+            out = np.zeros((ids.size, 64, 3), dtype=np.float32)
+            rc = ref.ref_render_tiles(ref_scene, int(integ), args.spp, ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                      ids.size, threads, out.ctypes.data_as(C.POINTER(C.c_float)))
+            assert rc == 0
+            return out
+        out, _ = _oracle.render(scene, integ, args.spp, ids, threads=threads, variant="glibc")
+        return out
+
+    done, t_used, chunk, tiles_out = [], 0.0, threads, []
     while t_used < args.cpu_seconds and len(done) < n_tiles:
-        ids = order[len(done):len(done) + chunk]
+        ids = np.ascontiguousarray(order[len(done):len(done) + chunk])
         t0 = time.perf_counter()
-        out, st = _oracle.render(scene, integ, args.spp, ids, threads=threads, variant="glibc")
+        tiles_out.append(run(ids))
         dt = time.perf_counter() - t0
         t_used += dt
-        rays += st["rays"]
-        samples += st["samples"]
         done.extend(ids.tolist())
-        tiles_out.append(out)
         if dt < args.cpu_seconds / 8:
             chunk *= 2
-    cpu = {"value": round(rays / t_used / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
-           "sample": f"{len(done)} random 8x8 tiles of the same frame @ {args.spp} spp ({samples} samples, "
-                     f"{t_used:.1f} s, oracle/liboracle_glibc.so)",
-           "msamples_per_s": round(samples / t_used / 1e6, 5)}
-    parity = None
+    if ref_scene:
+        ref.ref_scene_free(ref_scene)
+    ids = np.array(done, dtype=np.int32)
+    orc, st = _oracle.render(scene, integ, args.spp, ids, threads=threads, variant="glibc")
+    base = np.concatenate(tiles_out, axis=0)
+    cpu = {"value": round(st["rays"] / t_used / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": kind,
+           "sample": f"{len(done)} random 8x8 tiles of the same frame @ {args.spp} spp ({st['samples']} samples, "
+                     f"{t_used:.1f} s, " + ("oracle/_ref/libsp_ref.so = reference sources" if ref is not None
+                                             else "oracle liboracle_glibc.so") + ")",
+           "msamples_per_s": round(st["samples"] / t_used / 1e6, 5)}
+    parity = {"vs": kind, "tiles": len(done)}
+    if ref is not None:
+        parity["oracle_bitexact_vs_reference"] = bool(np.array_equal(orc.view(np.uint32), base.view(np.uint32)))
     if gpu_out is not None:
-        ref = np.concatenate(tiles_out, axis=0)
         gpu = gpu_out.cpu().numpy()
         pos = {int(t): i for i, t in enumerate(my_tiles)}
         g = np.stack([gpu[pos[t]] for t in done])
-        diff = np.linalg.norm((g - ref).ravel())
-        norm = np.linalg.norm(ref.ravel())
-        spm, _ = _oracle.render(scene, integ, args.spp, np.array(done[: min(len(done), 8)], dtype=np.int32),
-                                threads=threads, variant="spm")
-        parity = {"vs": "oracle(glibc libm)", "tiles": len(done), "rel_l2": float(diff / max(norm, 1e-30)),
-                  "bitexact_pixel_frac": float(np.mean(np.all(g == ref, axis=-1))),
-                  "bitexact_vs_spm_oracle": bool(np.array_equal(g[: spm.shape[0]], spm))}
+        diff = np.linalg.norm((g - base).ravel())
+        norm = np.linalg.norm(base.ravel())
+        parity.update({"rel_l2": float(diff / max(norm, 1e-30)),
+                       "bitexact_pixel_frac": float(np.mean(np.all(g == base, axis=-1)))})
     return cpu, parity
 
 

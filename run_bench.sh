@@ -1,11 +1,15 @@
 #!/bin/bash
+# Round bench session: GPU parity tests, the default bench line (with CPU baseline), and a
+# rocprofv3 kernel-trace summary of the same command.
 set -o pipefail
 cd "$(dirname "$0")"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 10 > gpurun_out/bench.json 2> gpurun_out/bench.err
-rc=$?; echo "bench exit $rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
-cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof.err
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; echo "bench exit $rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
+[ $rc -eq 0 ] || exit $rc
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof.err
 echo "rocprof exit $?"
-find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*stats*" | head

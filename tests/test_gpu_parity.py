@@ -137,3 +137,25 @@ def test_wavefront_rejects_other_integrators(scene_dir):
     s = load(scene_dir, "bunny.sp", 16, 16, bvh=0)
     with pytest.raises(sp.SimplePathError):
         sp.render_tiles(s, "iterative_rrnee", 1, pipeline="wavefront")
+
+
+@pytest.mark.parametrize("scene,w,h,integrator,spp", [("bunny.sp", 64, 40, "direct_lighting", 4),
+                                                      ("bunny.sp", 32, 24, "iterative_rrnee", 2),
+                                                      ("material_spheres.sp", 24, 48, "whitted", 3),
+                                                      ("material_spheres.sp", 24, 48, "brute_force_iterative_rr", 3)])
+def test_vs_reference_build_bitexact(scene_dir, scene, w, h, integrator, spp):
+    # the HIP path against the reference's own code (oracle/_ref, built from its sources)
+    from tests import test_oracle_vs_ref as R
+    if not os.path.exists(R.REF_LIB):
+        pytest.skip("oracle/_ref not built (reference sources were not available)")
+    import ctypes as C
+    L = C.CDLL(R.REF_LIB)
+    L.ref_render.restype = C.c_int
+    L.ref_render.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_uint32, C.POINTER(C.c_int32), C.c_int64,
+                             C.c_int, C.POINTER(C.c_float)]
+    L.ref_last_error.restype = C.c_char_p
+    s = load(scene_dir, scene, w, h, bvh=1)
+    g, _ = sp.render_tiles(s, integrator, spp)
+    ids = np.arange(g.shape[0], dtype=np.int32)
+    r = R.ref_render(L, os.path.join(scene_dir, scene), w, h, sp.string_to_integrator_type(integrator), spp, ids)
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), rel_l2(g, r)
