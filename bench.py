@@ -78,21 +78,24 @@ def main():
     scene.upload(device=local, bvh_mode=args.bvh)
     integ = sp.string_to_integrator_type(args.integrator)
 
+    from simplepath_amd import shard
+
     sched = sp.ColumnMajorTileScheduler(args.width, args.height)
     n_tiles = sched.get_num_tiles()
-    my_tiles = sched.shard(rank, world)
-    per_rank = (n_tiles + world - 1) // world
+    my_tiles = shard.shard_tiles(n_tiles, rank, world)
+    per_rank = shard.per_rank_capacity(n_tiles, world)
     out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
-    gathered = None
+    gathered, frame = None, None
     if dist is not None and rank == 0:
         gathered = [torch.zeros_like(out) for _ in range(world)]
+        frame = torch.zeros((n_tiles, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():
         st = sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
                                     pipeline=args.pipeline, stage_timing=True)
-        if dist is not None:
-            dist.gather(out, gathered if rank == 0 else None, dst=0)
+        if dist is not None:  # single RCCL gather of the tile buffers at frame end
+            shard.gather_frame(out, n_tiles, rank, world, dist, gathered, frame)
         return st
 
     for _ in range(args.warmup):

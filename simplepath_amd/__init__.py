@@ -150,8 +150,9 @@ class ColumnMajorTileScheduler(TileScheduler):
         return c % n
 
     def shard(self, rank: int, world: int) -> np.ndarray:
-        """Tiles owned by `rank` of `world` (interleaved: balanced cost across ranks)."""
-        return np.arange(rank, self.get_num_tiles(), world, dtype=np.int32)
+        """Tiles owned by `rank` of `world` (interleaved: balanced cost across ranks; shard.py)."""
+        from .shard import shard_tiles
+        return shard_tiles(self.get_num_tiles(), rank, world)
 
 
 PIPELINES = {"auto": 0, "megakernel": 1, "wavefront": 2}

@@ -1,0 +1,74 @@
+"""Multi-rank frame assembly on CPU (gloo, world_size 2): each rank renders its shard of tiles
+(here with the CPU oracle -- the GPU path is not available on CPU, the sharding / gather logic
+is the same code bench.py runs over RCCL), the frame-end gather brings them to rank 0, and the
+assembled frame must equal a single-process render of all tiles."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, scene_path, w, h, spp, result_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import simplepath_amd as sp
+    from simplepath_amd import shard
+    from tests import _oracle
+
+    scene = sp.Scene.from_file(scene_path)
+    scene.set_resolution(w, h)
+    n = sp.TileScheduler(w, h).get_num_tiles()
+    mine = shard.shard_tiles(n, rank, world)
+    local = torch.zeros((shard.per_rank_capacity(n, world), 64, 3), dtype=torch.float32)
+    tiles, _ = _oracle.render(scene, 6, spp, mine, threads=2, variant="glibc")
+    local[: len(mine)] = torch.from_numpy(tiles)
+    frame = shard.gather_frame(local, n, rank, world, dist)
+    if rank == 0:
+        np.save(result_path, frame.numpy())
+    else:
+        assert frame is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_frame_matches_single_process(scene_dir, tmp_path, world):
+    import simplepath_amd as sp
+    from tests import _oracle
+
+    w, h, spp = 40, 24, 2  # 15 tiles: ragged shards for world 2 (8 + 7) and world 3
+    path = os.path.join(scene_dir, "bunny.sp")
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), path, w, h, spp, out), nprocs=world,
+                       join=True, start_method="spawn")
+    frame = np.load(out)
+    scene = sp.Scene.from_file(path)
+    scene.set_resolution(w, h)
+    ref, _ = _oracle.render(scene, 6, spp, None, threads=4, variant="glibc")
+    assert frame.shape == ref.shape
+    assert np.array_equal(frame.view(np.uint32), ref.view(np.uint32))
+
+
+def test_shards_partition_the_frame():
+    from simplepath_amd import shard
+    for n in (1, 7, 32400):
+        for world in (1, 2, 3, 8):
+            parts = [shard.shard_tiles(n, r, world) for r in range(world)]
+            allt = np.sort(np.concatenate(parts))
+            assert np.array_equal(allt, np.arange(n))
+            assert max(len(p) for p in parts) == shard.per_rank_capacity(n, world)
