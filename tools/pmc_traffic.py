@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (run_pmc_traffic.sh).
+
+Correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reports half the bytes of coalesced reads on
+gfx950 -> doubled; WRITE_SIZE is exact.  Both are in KiB.  Calibrated on this code's own
+patterns: wf_init's 8-byte-per-lane MT seeding stores (known 2512 B per pixel) and wf_resolve's
+4-byte-per-lane reads (known 12 B per pixel) reproduce their byte counts with these factors.
+
+Usage: python3 tools/pmc_traffic.py <pmc dir with p1 (FETCH) and p2 (WRITE)> <width> <height> <spp> <out.json>
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(root, counter):
+    vals = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] == counter:
+                    vals[row["Kernel_Name"].split("(")[0]].append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    root, w, h, spp, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+    fetch = per_kernel(os.path.join(root, "p1"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(root, "p2"), "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        if not k.startswith("spd::"):
+            continue
+        f, wr = fetch.get(k, []), write.get(k, [])
+        n = max(len(f), len(wr), 1)
+        fb = 2.0 * 1024.0 * sum(f) / max(len(f), 1)
+        wb = 1024.0 * sum(wr) / max(len(wr), 1)
+        kernels[k.replace("spd::", "")] = {"dispatches": n, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                                           "hbm_bytes_per_launch": fb + wb}
+    dom = "wf_shade" if "wf_shade" in kernels else max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
+    res = {"width": w, "height": h, "spp": spp, "kernel": dom,
+           "hbm_bytes_per_launch": kernels[dom]["hbm_bytes_per_launch"], "kernels": kernels,
+           "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1, KiB -> bytes"}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
