@@ -449,6 +449,69 @@ __device__ __forceinline__ bool pair_any(const Scene& sc, const Ray& ray, float 
     return false;
 }
 
+// Wave-uniform record fetch through the constant address space: with the address in SGPRs
+// the compiler emits s_load (scalar cache).  A uniform-address VECTOR load still costs the
+// vector L1 a per-lane access (TCP_TOTAL_ACCESSES), which is what bounds the traversal kernels.
+// Only for records whose index is equal across the active lanes (loops over scene lists).
+typedef const __attribute__((address_space(4))) float    cf32;
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+__device__ __forceinline__ uintptr_t uptr(const void* p)
+{
+    const uint64_t a  = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    return (uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t uload_u32(const void* p) { return *(cu32*)uptr(p); }
+__device__ __forceinline__ f3 uload_f3(const f3* p)
+{
+    cf32* q = (cf32*)uptr(p);
+    return mk(q[0], q[1], q[2]);
+}
+__device__ __forceinline__ aff uload_aff(const aff* p)
+{
+    aff a;
+    a.vx = uload_f3(&p->vx);
+    a.vy = uload_f3(&p->vy);
+    a.vz = uload_f3(&p->vz);
+    a.p  = uload_f3(&p->p);
+    return a;
+}
+__device__ __forceinline__ Node uload_node(const Node* p)
+{
+    cu32* q = (cu32*)uptr(p);
+    Node  n;
+    n.lo[0] = __uint_as_float(q[0]); n.lo[1] = __uint_as_float(q[1]); n.lo[2] = __uint_as_float(q[2]); n.a = q[3];
+    n.hi[0] = __uint_as_float(q[4]); n.hi[1] = __uint_as_float(q[5]); n.hi[2] = __uint_as_float(q[6]); n.b = q[7];
+    return n;
+}
+// the fields of a sphere / sphere light that ray tests read
+struct UShape {
+    aff     w2o;
+    int32_t kind;
+};
+__device__ __forceinline__ UShape uload_shape(const Shape* p)
+{
+    UShape u;
+    u.w2o  = uload_aff(&p->w2o);
+    u.kind = (int32_t)uload_u32(&p->kind);
+    return u;
+}
+__device__ __forceinline__ Light uload_light(const Light* p)
+{
+    Light l;
+    l.kind     = (int32_t)uload_u32(&p->kind);
+    l.pad      = 0;
+    const f3 r = uload_f3(reinterpret_cast<const f3*>(&p->radiance));
+    l.radiance = mkc(r.x, r.y, r.z);
+    l.o2w      = uload_aff(&p->o2w);
+    l.w2o      = uload_aff(&p->w2o);
+    l.nrm.vx   = uload_f3(&p->nrm.vx);
+    l.nrm.vy   = uload_f3(&p->nrm.vy);
+    l.nrm.vz   = uload_f3(&p->nrm.vz);
+    return l;
+}
+
 // Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
 __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
@@ -456,10 +519,10 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
     h.t    = tmax;
     h.code = 0xffffffffu;
     for (int i = 0; i < sc.n_unbounded; ++i) {
-        const int    sid = sc.unbounded[i];
-        const Shape& s   = sc.shapes[sid];
+        const int    sid = (int)uload_u32(sc.unbounded + i);
+        const UShape s   = uload_shape(sc.shapes + sid);
         float        t;
-        const bool   hit = (s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
+        const bool  hit = (s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
         if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
     if (sc.n_nodes == 0) return h;
@@ -499,7 +562,7 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
 __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     for (int i = 0; i < sc.n_unbounded; ++i) {
-        const Shape& s = sc.shapes[sc.unbounded[i]];
+        const UShape s = uload_shape(sc.shapes + uload_u32(sc.unbounded + i));
         float        t;
         if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
     }
@@ -548,7 +611,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
     lh.hit = false;
     lh.t   = tmax;
     for (int i = 0; i < sc.n_unbounded_lights; ++i) {
-        const Light& l = sc.lights[sc.unbounded_lights[i]];
+        const Light l = uload_light(sc.lights + uload_u32(sc.unbounded_lights + i));
         // EnvironmentLight::intersect_lights_impl (Lights/Light.h:242)
         if (!(lh.t < k_infinite)) {
             lh.hit = true;
@@ -557,6 +620,22 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
         }
     }
     if (sc.n_light_nodes == 0) return lh;
+    if (sc.n_light_nodes == 1) { // a single leaf (root: no box test): the same lights for every lane
+        const Node     n   = uload_node(sc.light_nodes);
+        const uint32_t cnt = n.b & ~LEAF_BIT;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const Light* lp = sc.lights + uload_u32(sc.light_slot + n.a + k);
+            const aff    w2o = uload_aff(&lp->w2o);
+            float        t;
+            if (sphere_t(w2o, ray, tmin, lh.t, t)) {
+                const f3 r = uload_f3(reinterpret_cast<const f3*>(&lp->radiance));
+                lh.hit = true;
+                lh.t   = t;
+                lh.L   = mkc(r.x, r.y, r.z);
+            }
+        }
+        return lh;
+    }
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     int      sp  = 0;
     uint32_t cur = 0;
@@ -594,6 +673,16 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
 __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     if (sc.n_light_nodes == 0) return false; // environment lights never occlude
+    if (sc.n_light_nodes == 1) {
+        const Node     n   = uload_node(sc.light_nodes);
+        const uint32_t cnt = n.b & ~LEAF_BIT;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const aff w2o = uload_aff(&sc.lights[uload_u32(sc.light_slot + n.a + k)].w2o);
+            float     t;
+            if (sphere_t(w2o, ray, tmin, tmax, t)) return true;
+        }
+        return false;
+    }
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     int      sp  = 0;
     uint32_t cur = 0;
@@ -1191,7 +1280,7 @@ __device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
 {
     rgb L = mkc(0, 0, 0);
     for (int li = 0; li < c.sc.n_lights; ++li) {
-        const Light&  l  = c.sc.lights[li];
+        const Light   l  = uload_light(c.sc.lights + li);
         const LSample ls = light_sample(l, is.p, is.n, next2D(c.rng), c.q);
         if (ls.pdf == 0.0f || cblack(ls.L)) continue;
         const f3  wi = ls.ray.d;

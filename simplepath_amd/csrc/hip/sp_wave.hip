@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(WF_BLOCK, 3) wf_shade(Scene sc, WaveArgs w, ui
             const Isect is  = finish_hit(sc, h, ray, q);
             const f3    wo  = neg(ray.d);
             for (int li = 0; li < sc.n_lights; ++li) {
-                const Light&  l  = sc.lights[li];
+                const Light   l  = uload_light(sc.lights + li);
                 const LSample ls = light_sample(l, is.p, is.n, next2D(rng), q);
                 if (ls.pdf == 0.0f || cblack(ls.L)) continue;
                 const f3  wi = ls.ray.d;
