@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -100,6 +101,61 @@ std::vector<float4> pair_nodes(const sph::Bvh& bvh)
         q[2] = make_float4(R.lo[2], R.hi[0], R.hi[1], R.hi[2]);
         q[3] = make_float4(u2f(ref_of(l)), u2f(ref_of(r)), u2f(n.a >> sph::BVH_AXIS_SHIFT), 0.0f);
     }
+    return out;
+}
+
+// 16-byte quantised copy of a binary SAH BVH (sp_path.hpp qnode_*): boxes as 16-bit offsets
+// from the root box on a per-axis grid, rounded outward so every decoded box (decoded on the
+// device as fmaf(q, scale, origin), here with the same fused operation) contains its exact box;
+// siblings adjacent, so a node is {lo.xyz, hi.xyz as u16, meta} with meta = first child | axis
+// << 29, or QLEAF | count << 28 | first slot.
+std::vector<uint4> quantized_nodes(const sph::Bvh& bvh, float origin[3], float scale[3])
+{
+    const auto& bn = bvh.nodes;
+    for (int a = 0; a < 3; ++a) {
+        const float lo = bn[0].lo[a], hi = bn[0].hi[a];
+        float       s  = (hi > lo) ? (hi - lo) / 65535.0f : 1e-30f;
+        while (std::fmaf(65535.0f, s, lo) < hi) s = std::nextafterf(s, INFINITY);
+        origin[a] = lo;
+        scale[a]  = s;
+    }
+    auto qlo = [&](int a, float v) -> uint32_t {
+        double   f = std::floor(((double)v - origin[a]) / scale[a]);
+        uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, f));
+        while (q > 0 && std::fmaf((float)q, scale[a], origin[a]) > v) --q;
+        return q;
+    };
+    auto qhi = [&](int a, float v) -> uint32_t {
+        double   f = std::ceil(((double)v - origin[a]) / scale[a]);
+        uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, f));
+        while (q < 65535 && std::fmaf((float)q, scale[a], origin[a]) < v) ++q;
+        return q;
+    };
+    std::vector<uint4> out(bn.size());
+    std::vector<std::pair<uint32_t, uint32_t>> todo{ { 0u, 0u } }; // (binary node, output slot)
+    uint32_t next = 1;
+    while (!todo.empty()) {
+        const auto [i, k] = todo.back();
+        todo.pop_back();
+        const auto& n = bn[i];
+        uint32_t    q[6];
+        for (int a = 0; a < 3; ++a) { q[a] = qlo(a, n.lo[a]); q[3 + a] = qhi(a, n.hi[a]); }
+        uint32_t meta;
+        if (n.b & sph::BVH_LEAF) {
+            const uint32_t cnt = n.b & ~sph::BVH_LEAF;
+            if (cnt > 7 || n.a > 0x0fffffffu) throw std::runtime_error("leaf does not fit a quantized node");
+            meta = spd::QLEAF | (cnt << 28) | n.a;
+        } else {
+            const uint32_t first = next;
+            next += 2;
+            if (first > 0x1fffffffu) throw std::runtime_error("too many nodes for a quantized BVH");
+            meta = first | ((n.a >> sph::BVH_AXIS_SHIFT) << 29);
+            todo.push_back({ n.b, first + 1 });
+            todo.push_back({ n.a & sph::BVH_CHILD_MASK, first });
+        }
+        out[k] = make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), meta);
+    }
+    out.resize(next);
     return out;
 }
 
@@ -484,6 +540,12 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
         const bool use_pairs = std::getenv("SP_PAIRS") && std::atoi(std::getenv("SP_PAIRS")) != 0;
         if (use_pairs) pairs = pair_nodes(bvh);
     }
+    std::vector<uint4> qnodes; // SAH: 16-byte quantised nodes (opt-in SP_QNODES=1: slower on the bunny frame)
+    float              qo[3] = { 0, 0, 0 }, qs[3] = { 0, 0, 0 };
+    if (bvh_mode != 1 && !nodes.empty() && pairs.empty()) {
+        const bool use_q = std::getenv("SP_QNODES") && std::atoi(std::getenv("SP_QNODES")) != 0;
+        if (use_q) qnodes = quantized_nodes(bvh, qo, qs);
+    }
 
     // ---- lights: Scene::m_lights order + accelerator (partition by boundedness)
     std::vector<spd::Light> lights;
@@ -526,6 +588,9 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     up(nodes, &d.nodes);
     d.pairs = nullptr;
     if (!pairs.empty()) up(pairs, &d.pairs);
+    d.qnodes = nullptr;
+    if (!qnodes.empty()) up(qnodes, &d.qnodes);
+    for (int a = 0; a < 3; ++a) { d.qorigin[a] = qo[a]; d.qscale[a] = qs[a]; }
     up(slot_tri, &d.slot_tri);
     up(slot_code, &d.slot_code);
     std::vector<float> nrm(h.normals.size() * 3);
@@ -621,10 +686,13 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         double budget_gb = 64.0;
         if (const char* v = std::getenv("SP_WAVE_MAX_GB")) budget_gb = std::atof(v);
         const size_t  per_pix   = spd::wave_bytes_per_pixel(s->dev.n_lights);
-        const int64_t max_tiles = std::max<int64_t>(1, (int64_t)(budget_gb * 1e9 / (double)(per_pix * 64)));
+        // queue items pack the pixel slot in 27 bits (sp_wave.hip wf_shade)
+        const int64_t max_tiles = std::min<int64_t>((int64_t)1 << 21,
+                                                    std::max<int64_t>(1, (int64_t)(budget_gb * 1e9 / (double)(per_pix * 64))));
         const int64_t chunk     = std::min<int64_t>(n_tiles, max_tiles);
         const size_t  n         = (size_t)chunk * 64;
-        const size_t  need      = n * per_pix + spd::wave_stat_bytes((int64_t)n) + spd::wave_queue_bytes((int64_t)n) + 256 * 10;
+        const size_t  need      = n * per_pix + spd::wave_stat_bytes((int64_t)n) + spd::wave_queue_bytes((int64_t)n, s->dev.n_lights) +
+                                  n * (size_t)std::max(1, s->dev.n_lights) + 256 * 12;
         if (need > s->wave_cap) {
             if (s->wave_buf) (void)hipFree(s->wave_buf);
             s->wave_buf = nullptr;
@@ -645,8 +713,9 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         w.shp      = reinterpret_cast<float4*>(take(n * 16));
         w.acc      = reinterpret_cast<float*>(take(n * 12));
         w.rstate   = reinterpret_cast<uint32_t*>(take(n * 4));
-        w.queue    = reinterpret_cast<uint32_t*>(take(spd::wave_queue_bytes((int64_t)n)));
-        w.qcount   = w.queue + (spd::wave_queue_bytes((int64_t)n) / 4 - 32 * 32);
+        w.queue    = reinterpret_cast<uint32_t*>(take(spd::wave_queue_bytes((int64_t)n, s->dev.n_lights)));
+        w.qcount   = nullptr; // per part (wave_render)
+        w.vis      = reinterpret_cast<uint8_t*>(take(n * (size_t)std::max(1, s->dev.n_lights)));
         w.wstat    = reinterpret_cast<unsigned long long*>(take(spd::wave_stat_bytes((int64_t)n)));
         w.counters = s->counters;
         // SP_WAVE_DIAG=<file>: per-wave timeline of one sample's primary + shadow launches
@@ -698,7 +767,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
             SP_HIP(spd::wave_render(s->dev, w, d_out + (size_t)t0 * 64 * 3, per_cu, s->n_cu, stream,
                                     timing ? s->stage_ev.data() : nullptr, n_parts > 1 ? s->aux_stream : nullptr,
                                     s->ev_fork, s->ev_join, s->ev_shade, &parts_used));
-            launches += 3 + 3 * (int)w.spp;
+            launches += 3 + 4 * (int)w.spp;
             if (d_diag) {
                 std::vector<unsigned long long> h(diag_n);
                 SP_HIP(hipStreamSynchronize(stream));

@@ -27,6 +27,7 @@ constexpr uint32_t AXIS_SHIFT = 30;                      // sp_host.hpp BVH_AXIS
 constexpr uint32_t CHILD_MASK = (1u << AXIS_SHIFT) - 1u;
 constexpr uint32_t PLEAF      = 0x80000000u; // pair-node child reference: leaf flag
 constexpr uint32_t PNONE      = 0xffffffffu; // pair-node child reference: no child
+constexpr uint32_t QLEAF      = 0x80000000u; // quantised node meta: leaf flag
 
 struct Node {
     float    lo[3];
@@ -69,6 +70,8 @@ struct Scene {
     int             n_nodes;
     const Node*     nodes;
     const float4*   pairs;     // pair-node copy of an SAH BVH (sp_path.hpp), nullptr otherwise
+    const uint4*    qnodes;    // 16-byte quantised copy of an SAH BVH (sp_path.hpp), nullptr otherwise
+    float           qorigin[3], qscale[3];
     const float4*   slot_tri;  // 3 per slot
     const uint32_t* slot_code;
     const float*    normals;   // 3 per vertex

@@ -449,6 +449,91 @@ __device__ __forceinline__ bool pair_any(const Scene& sc, const Ray& ray, float 
     return false;
 }
 
+
+// ------------------------------------------------------------------------------ quantised BVH
+// 16-byte nodes: one dwordx4 fetch per visited node instead of two.  Boxes decode to a
+// superset of the exact boxes (outward rounding at build time), so the walk may visit a few
+// more nodes but never misses one; like near-first order this can only change which of two
+// primitives at exactly equal distance wins, so the reference-order BVH never uses it.
+__device__ __forceinline__ bool qbox_hit(const Scene& sc, const uint4& q, const Ray& r, const f3& inv, float tmin,
+                                         float tmax)
+{
+    Node n;
+    n.lo[0] = fma_f((float)(q.x & 0xffffu), sc.qscale[0], sc.qorigin[0]);
+    n.lo[1] = fma_f((float)(q.x >> 16), sc.qscale[1], sc.qorigin[1]);
+    n.lo[2] = fma_f((float)(q.y & 0xffffu), sc.qscale[2], sc.qorigin[2]);
+    n.hi[0] = fma_f((float)(q.y >> 16), sc.qscale[0], sc.qorigin[0]);
+    n.hi[1] = fma_f((float)(q.z & 0xffffu), sc.qscale[1], sc.qorigin[1]);
+    n.hi[2] = fma_f((float)(q.z >> 16), sc.qscale[2], sc.qorigin[2]);
+    return box_hit(n, r, inv, tmin, tmax);
+}
+__device__ __forceinline__ bool q_near_is_second(uint32_t meta, const f3& d)
+{
+    const uint32_t ax = (meta >> 29) & 3u;
+    const float    da = (ax == 0) ? d.x : ((ax == 1) ? d.y : d.z);
+    return da < 0.0f;
+}
+
+__device__ __forceinline__ void qnode_closest(const Scene& sc, const Ray& ray, float tmin, Hit& h, Stack st)
+{
+    const f3 inv      = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp       = 0;
+    uint32_t cur      = 0; // root: no box test
+    bool     test_box = false;
+    while (true) {
+        const uint4 q = sc.qnodes[cur];
+        if (!test_box || qbox_hit(sc, q, ray, inv, tmin, h.t)) {
+            if (q.w & QLEAF) {
+                const uint32_t first = q.w & 0x0fffffffu, cnt = (q.w >> 28) & 7u;
+                for (uint32_t k = 0; k < cnt; ++k) prim_closest(sc, first + k, ray, tmin, h);
+            } else {
+                const uint32_t c0 = q.w & 0x1fffffffu;
+                const bool     sw = q_near_is_second(q.w, ray.d);
+                st.s[sp * 64 + st.lane] = sw ? c0 : c0 + 1;
+                ++sp;
+                cur      = sw ? c0 + 1 : c0;
+                test_box = true;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur      = st.s[sp * 64 + st.lane];
+        test_box = true;
+    }
+}
+
+__device__ __forceinline__ bool qnode_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    const f3 inv      = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp       = 0;
+    uint32_t cur      = 0;
+    bool     test_box = false;
+    while (true) {
+        const uint4 q = sc.qnodes[cur];
+        if (!test_box || qbox_hit(sc, q, ray, inv, tmin, tmax)) {
+            if (q.w & QLEAF) {
+                const uint32_t first = q.w & 0x0fffffffu, cnt = (q.w >> 28) & 7u;
+                for (uint32_t k = 0; k < cnt; ++k)
+                    if (prim_any(sc, first + k, ray, tmin, tmax)) return true;
+            } else {
+                const uint32_t c0 = q.w & 0x1fffffffu;
+                const bool     sw = q_near_is_second(q.w, ray.d);
+                st.s[sp * 64 + st.lane] = sw ? c0 : c0 + 1;
+                ++sp;
+                cur      = sw ? c0 + 1 : c0;
+                test_box = true;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur      = st.s[sp * 64 + st.lane];
+        test_box = true;
+    }
+    return false;
+}
+
 // Wave-uniform record fetch through the constant address space: with the address in SGPRs
 // the compiler emits s_load (scalar cache).  A uniform-address VECTOR load still costs the
 // vector L1 a per-lane access (TCP_TOTAL_ACCESSES), which is what bounds the traversal kernels.
@@ -526,6 +611,10 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
         if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
     if (sc.n_nodes == 0) return h;
+    if (sc.qnodes) {
+        qnode_closest(sc, ray, tmin, h, st);
+        return h;
+    }
     if (sc.pairs) {
         pair_closest(sc, ray, tmin, h, st);
         return h;
@@ -567,6 +656,7 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
         if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
     }
     if (sc.n_nodes == 0) return false;
+    if (sc.qnodes) return qnode_any(sc, ray, tmin, tmax, st);
     if (sc.pairs) return pair_any(sc, ray, tmin, tmax, st);
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     int      sp  = 0;

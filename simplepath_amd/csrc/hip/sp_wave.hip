@@ -36,6 +36,7 @@ namespace spd {
 constexpr int WF_BLOCK = 256;
 constexpr int QSEG     = 32; // shadow-queue segments (one counter each, QSTRIDE words apart)
 constexpr int QSTRIDE  = 32;
+constexpr int QFETCH   = 16; // fetch counter of a segment: QFETCH words after its fill counter
 __host__ __device__ inline size_t qseg_cap(int64_t n) { return (size_t)64 * (size_t)(((n >> 6) + QSEG - 1) / QSEG); }
 
 struct PixelRef {
@@ -152,7 +153,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uin
     extern __shared__ uint32_t lds[];
     const int64_t p    = w.pb + (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
     const int     lane = threadIdx.x & 63;
-    if (blockIdx.x == 0 && threadIdx.x < QSEG) w.qcount[threadIdx.x * QSTRIDE] = 0u; // previous wf_shadow is done
+    if (blockIdx.x == 0 && threadIdx.x < QSEG) { // previous sample's shadow kernels are done
+        w.qcount[threadIdx.x * QSTRIDE]          = 0u;
+        w.qcount[threadIdx.x * QSTRIDE + QFETCH] = 0u;
+    }
     if (p >= w.pe) return;
     const uint64_t t0 = w.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t       steps = 0;
@@ -240,23 +244,31 @@ __global__ void __launch_bounds__(WF_BLOCK, 3) wf_shade(Scene sc, WaveArgs w, ui
         draws = rng.draws;
         rng_store(w, p, rng);
     }
-    // active-ray compaction: wave ballot + prefix popcount, one atomic per wave on one of QSEG
-    // segment counters (tile slot % QSEG) so that no single address serialises the chip
-    const unsigned long long ballot = __ballot(mask != 0);
-    if (ballot) {
-        const int      lane  = threadIdx.x & 63;
-        const uint32_t total = (uint32_t)__popcll(ballot);
-        const uint32_t seg   = (uint32_t)(p >> 6) % QSEG;
-        uint32_t       base  = 0;
+    // Active-ray compaction: every (pixel, light) shadow ray becomes one queue item
+    // (p << 5 | light).  Wave prefix sum of the per-lane counts, one atomic per wave on one of
+    // QSEG segment counters (tile slot % QSEG) so that no single address serialises the chip.
+    const int      lane = threadIdx.x & 63;
+    const uint32_t mine = (uint32_t)__popc(mask);
+    uint32_t       incl = mine;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (total) {
+        const uint32_t seg  = (uint32_t)(p >> 6) % QSEG;
+        uint32_t       base = 0;
         if (lane == 0) base = atomicAdd(w.qcount + seg * QSTRIDE, total);
-        base = __shfl(base, 0, 64);
-        if (mask)
-            w.queue[(size_t)seg * w.qcap + base + (uint32_t)__popcll(ballot & ((1ull << lane) - 1ull))] = (uint32_t)p;
+        base            = __shfl(base, 0, 64);
+        uint32_t* out   = w.queue + (size_t)seg * w.qcap + base + (incl - mine);
+        uint32_t  k     = 0;
+        for (uint32_t m = mask; m; m &= m - 1) out[k++] = ((uint32_t)p << 5) | (uint32_t)(__ffs(m) - 1);
     }
     wave_count(w.wstat + (size_t)(p >> 6) * ST_N, ST_DRAWS, draws);
 }
 
-// Shadow queries + accumulation: direct_nee's occlusion half (Integrator.cpp:297-300).
+// Shadow queries, one queued ray per lane (static assignment; SP_SHADOW_DYN=0): direct_nee's
+// occlusion test (Integrator.cpp:297) -> vis[light][pixel].
 __global__ void __launch_bounds__(WF_BLOCK) wf_shadow(Scene sc, WaveArgs w)
 {
     extern __shared__ uint32_t lds[];
@@ -278,46 +290,176 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_shadow(Scene sc, WaveArgs w)
         const uint32_t j    = v % QSEG;
         const uint32_t k    = (v / QSEG) * 64 + (uint32_t)lane;
         const bool     live = k < (uint32_t)__shfl(segn, (int)j, 64);
-        const int64_t  p    = live ? (int64_t)w.queue[(size_t)j * cap + k] : 0;
+        const uint32_t item = live ? w.queue[(size_t)j * cap + k] : 0u;
+        const int64_t  p    = item >> 5;
+        const uint32_t li   = item & 31u;
         float4         o    = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (live) o = w.shp[p];
-        const uint32_t mask = __float_as_uint(o.w);
-        rgb            L    = mkc(0, 0, 0);
-        for (int li = 0; li < sc.n_lights; ++li) {
-            const bool on = live && ((mask >> li) & 1u);
-            if (!__any(on)) continue;
-            float4 d = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (on) {
-                const float4* e = w.sh + ((size_t)li * w.n + p) * 2;
-                d               = e[0];
-                c               = e[1];
-            }
-            Ray r;
-            r.o = mk(o.x, o.y, o.z);
-            r.d = mk(d.x, d.y, d.z);
-            bool occ;
-            if (sc.packet) {
-                occ = scene_any_w(sc, r, d.w, c.w, on, w.diag ? &steps : nullptr);
-            } else {
-                occ = on ? scene_any(sc, r, d.w, c.w, st) : true;
-            }
-            if (on) {
-                ++shadow;
-                if (!occ) L = cadd(L, mkc(c.x, c.y, c.z));
-            }
+        float4         d = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (live) {
+            o               = w.shp[p];
+            const float4* e = w.sh + ((size_t)li * w.n + p) * 2;
+            d               = e[0];
+            c               = e[1];
+        }
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        bool occ;
+        if (sc.packet) {
+            occ = scene_any_w(sc, r, d.w, c.w, live, w.diag ? &steps : nullptr);
+        } else {
+            occ = live ? scene_any(sc, r, d.w, c.w, st) : true;
         }
         if (live) {
-            w.acc[p]           = w.acc[p] + L.r;
-            w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
-            w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
+            ++shadow;
+            w.vis[(size_t)li * w.n + p] = occ ? 0 : 1;
         }
     }
     if (w.diag)
         diag_record(w.diag + ((size_t)(w.n >> 6) + (w.pb >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * 4, t0, steps,
                     (uint32_t)__popcll(__ballot(shadow != 0)));
-    unsigned long long* slot = w.wstat + ((size_t)(w.n >> 6) + (w.pb >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * ST_N;
+    unsigned long long* slot = w.wstat + ((size_t)w.sh_slot0 + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * ST_N;
     wave_count(slot, ST_RAYS, shadow); // occluded() counts the query as a ray too
     wave_count(slot, ST_SHADOW, shadow);
+}
+
+// Shadow queries with dynamic ray fetch: persistent waves whose lanes each trace one queued
+// shadow ray (Scene::intersect_p, Scene.h:79) and take a new one as soon as theirs finishes.
+// The rays of a 64-ray batch differ in length by 10x and more (unoccluded rays cross the scene,
+// occluded ones stop at the first hit), so a wave that waited for its slowest ray left ~75 % of
+// its lanes idle (profiles/r01: lane utilisation 0.25).  Refills take a batch of items from one
+// queue segment with one atomic per wave; a wave drains its own segment, then moves on.
+// Result: vis[light][pixel] = 1 when the ray reaches the light (order-free: wf_accum sums in
+// light order).  Opt-in (SP_SHADOW_DYN=1): on the bunny frame it is 2x SLOWER than the static
+// assignment -- refilled lanes sit at different depths of the tree, so the node fetches of a
+// wave stop coalescing, and the vector L1 is what bounds traversal.
+constexpr uint32_t SHADOW_REFILL = 16; // refill when at least this many lanes are idle
+
+__global__ void __launch_bounds__(WF_BLOCK) wf_shadow_dyn(Scene sc, WaveArgs w)
+{
+    extern __shared__ uint32_t lds[];
+    const int      lane   = threadIdx.x & 63;
+    const Stack    st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
+    const uint32_t wave_g = (blockIdx.x * WF_BLOCK + threadIdx.x) >> 6;
+    uint32_t       seg    = wave_g % QSEG;
+    int            left   = QSEG; // segments not yet found empty by this wave
+    bool           busy   = false;
+    uint32_t       item = 0, cur = 0;
+    int            sp = 0;
+    bool           test_box = false;
+    Ray            r;
+    f3             inv  = mk(0, 0, 0);
+    float          tmin = 0.0f, tmax = 0.0f;
+    uint32_t       shadow = 0;
+    const uint64_t lt     = (1ull << lane) - 1ull;
+    while (true) {
+        const uint64_t idle = __ballot(!busy);
+        if (left > 0 && (uint32_t)__popcll(idle) >= SHADOW_REFILL) {
+            const uint32_t want = (uint32_t)__popcll(idle);
+            uint32_t       base = 0, got = 0;
+            while (left > 0) {
+                const uint32_t segn = w.qcount[seg * QSTRIDE];
+                uint32_t       b    = 0;
+                if (lane == 0) b = atomicAdd(w.qcount + seg * QSTRIDE + QFETCH, want);
+                b = __shfl(b, 0, 64);
+                if (b < segn) {
+                    base = b;
+                    got  = min(want, segn - b);
+                    break;
+                }
+                seg = (seg + 1) % QSEG;
+                --left;
+            }
+            const uint32_t rank = (uint32_t)__popcll(idle & lt);
+            if (!busy && rank < got) {
+                item              = w.queue[(size_t)seg * w.qcap + base + rank];
+                const int64_t  p  = item >> 5;
+                const uint32_t li = item & 31u;
+                const float4   o  = w.shp[p];
+                const float4*  e  = w.sh + ((size_t)li * w.n + p) * 2;
+                const float4   d  = e[0];
+                const float4   c  = e[1];
+                r.o  = mk(o.x, o.y, o.z);
+                r.d  = mk(d.x, d.y, d.z);
+                tmin = d.w;
+                tmax = c.w;
+                ++shadow;
+                // unbounded geometry and the lights first (any order gives the same answer)
+                bool occ = false;
+                for (int i = 0; i < sc.n_unbounded && !occ; ++i) {
+                    const UShape u = uload_shape(sc.shapes + uload_u32(sc.unbounded + i));
+                    float        t;
+                    occ = (u.kind == SP_PRIM_SPHERE) ? sphere_t(u.w2o, r, tmin, tmax, t) : plane_t(u.w2o, r, tmin, tmax, t);
+                }
+                if (!occ) occ = lights_any(sc, r, tmin, tmax, st);
+                if (occ || sc.n_nodes == 0) {
+                    w.vis[(size_t)li * w.n + p] = occ ? 0 : 1;
+                } else {
+                    busy     = true;
+                    inv      = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+                    cur      = 0; // root: no box test
+                    sp       = 0;
+                    test_box = false;
+                }
+            }
+        }
+        if (__ballot(busy) == 0) {
+            if (left == 0) break;
+            continue;
+        }
+        if (busy) { // one node of BVHAccelerator::intersect_p (BVHAccelerator.h:62-77)
+            const Node n    = sc.nodes[cur];
+            bool       next = false, occ = false;
+            if (!test_box || box_hit(n, r, inv, tmin, tmax)) {
+                if (n.b & LEAF_BIT) {
+                    const uint32_t cnt = n.b & ~LEAF_BIT;
+                    for (uint32_t k = 0; k < cnt && !occ; ++k) occ = prim_any(sc, n.a + k, r, tmin, tmax);
+                } else {
+                    uint32_t first = n.a & CHILD_MASK, second = n.b;
+                    if (sc.ordered && near_is_second(n.a, r.d)) { const uint32_t t = first; first = second; second = t; }
+                    st.s[sp * 64 + st.lane] = second;
+                    ++sp;
+                    cur      = first;
+                    test_box = true;
+                    next     = true;
+                }
+            }
+            if (!next) {
+                if (occ || sp == 0) {
+                    w.vis[(size_t)(item & 31u) * w.n + (item >> 5)] = occ ? 0 : 1;
+                    busy = false;
+                } else {
+                    --sp;
+                    cur      = st.s[sp * 64 + st.lane];
+                    test_box = true;
+                }
+            }
+        }
+    }
+    unsigned long long* slot = w.wstat + ((size_t)w.sh_slot0 + wave_g) * ST_N;
+    wave_count(slot, ST_RAYS, shadow); // occluded() counts the query as a ray too
+    wave_count(slot, ST_SHADOW, shadow);
+}
+
+// direct_nee's sum (Integrator.cpp:300): L = unoccluded contributions in light order; sum += L.
+__global__ void __launch_bounds__(WF_BLOCK) wf_accum(Scene sc, WaveArgs w)
+{
+    const int64_t p = w.pb + (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
+    if (p >= w.pe) return;
+    if (__float_as_uint(w.hit[p].y) == 0xffffffffu) return; // no geometry hit this sample
+    const uint32_t mask = __float_as_uint(w.shp[p].w);
+    if (!mask) return;
+    rgb L = mkc(0, 0, 0);
+    for (uint32_t m = mask; m; m &= m - 1) {
+        const int li = __ffs(m) - 1;
+        if (w.vis[(size_t)li * w.n + p]) {
+            const float4 c = w.sh[((size_t)li * w.n + p) * 2 + 1];
+            L              = cadd(L, mkc(c.x, c.y, c.z));
+        }
+    }
+    w.acc[p]           = w.acc[p] + L.r;
+    w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
+    w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
 }
 
 __global__ void __launch_bounds__(WF_BLOCK) wf_resolve(Scene sc, WaveArgs w, float* out)
@@ -356,6 +498,11 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_stats(WaveArgs w, int64_t n_slots
 }
 
 // ---------------------------------------------------------------------------- host side
+static bool shadow_dyn_env()
+{
+    const char* v = std::getenv("SP_SHADOW_DYN"); // opt-in: slower on coherent shadow rays
+    return v ? std::atoi(v) != 0 : false;
+}
 static int32_t interleave_block_env()
 {
     const char* v = std::getenv("SP_WAVE_ILV");
@@ -373,9 +520,14 @@ size_t wave_bytes_per_pixel(int n_lights)
     return 3 * 4 + 4 + 16 + 16 + (size_t)n_lights * 32 + 4 + 2 * MT_N * 8;
 }
 // primary/shade/resolve slots (one per tile) + persistent shadow-wave slots (at most as many)
-size_t wave_stat_bytes(int64_t n) { return (size_t)2 * (size_t)(n >> 6) * ST_N * 8; }
+// tile slots + persistent shadow-wave slots of both parts (each part's grid is at most
+// ceil(part pixels / WF_BLOCK) blocks of WF_BLOCK / 64 waves)
+size_t wave_stat_bytes(int64_t n) { return (size_t)(2 * (size_t)(n >> 6) + 8) * ST_N * 8; }
 // room for up to two parts (wave_render), each QSEG segments + QSEG counters
-size_t wave_queue_bytes(int64_t n) { return 2 * (QSEG * (qseg_cap(n) + 64) + QSEG * QSTRIDE) * 4; }
+size_t wave_queue_bytes(int64_t n, int n_lights)
+{
+    return 2 * (QSEG * (qseg_cap(n) * (size_t)std::max(1, n_lights) + 64) + QSEG * QSTRIDE) * 4;
+}
 
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
                        hipStream_t stream, hipEvent_t* ev, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
@@ -406,7 +558,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         pw[k]            = wa;
         pw[k].pb         = s0 * 64;
         pw[k].pe         = (s0 + ns) * 64;
-        pw[k].qcap       = qseg_cap(ns * 64);
+        pw[k].qcap       = qseg_cap(ns * 64) * (size_t)std::max(1, sc.n_lights); // one item per (pixel, light)
         pw[k].queue      = q;
         pw[k].qcount     = q + QSEG * pw[k].qcap;
         q += QSEG * pw[k].qcap + QSEG * QSTRIDE;
@@ -421,12 +573,15 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         (void)hipStreamWaitEvent(aux, fork, 0);
     }
     const uint32_t diag_sample = diag_sample_env();
+    const bool     dyn         = shadow_dyn_env();
     unsigned       grid[2], sgrid[2];
     WaveArgs       pd[2];
     for (int k = 0; k < parts; ++k) {
         grid[k]  = (unsigned)((pw[k].pe - pw[k].pb + WF_BLOCK - 1) / WF_BLOCK);
         // the shadow queue never exceeds the part: a persistent grid sized to fill the chip
         sgrid[k] = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid[k], (int64_t)n_cu * traverse_blocks_per_cu));
+        // statistics slots of this part's persistent shadow waves, after the tile slots
+        pw[k].sh_slot0 = (w.n >> 6) + (k == 0 ? 0 : (int64_t)sgrid[0] * (WF_BLOCK / 64));
         pd[k]      = pw[k]; // diagnostics: only the launches of sample diag_sample record
         pd[k].diag = nullptr;
     }
@@ -443,7 +598,9 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
             hipLaunchKernelGGL(wf_shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, pd[k], i);
             if (parts > 1) (void)hipEventRecord(shade_done[k], st);
             if (k == 0) mark();
-            hipLaunchKernelGGL(wf_shadow, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
+            if (dyn) hipLaunchKernelGGL(wf_shadow_dyn, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
+            else hipLaunchKernelGGL(wf_shadow, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
+            hipLaunchKernelGGL(wf_accum, dim3(grid[k]), dim3(WF_BLOCK), 0, st, sc, wi);
             if (k == 0) mark();
         }
     }
@@ -452,7 +609,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         (void)hipStreamWaitEvent(stream, join, 0);
     }
     hipLaunchKernelGGL(wf_resolve, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, wa, out);
-    const int64_t n_slots = 2 * slots;
+    const int64_t n_slots = 2 * slots + 8;
     hipLaunchKernelGGL(wf_stats, dim3(64), dim3(WF_BLOCK), 0, stream, w, n_slots);
     mark();
     return hipGetLastError();

@@ -18,12 +18,14 @@ struct WaveArgs {
     float4*             hit;       // [n]
     float4*             shp;       // [n]
     float4*             sh;        // [n_lights][n][2]
+    uint8_t*            vis;       // [n_lights][n] shadow ray reached the light
     uint32_t*           queue;     // QSEG segments (sp_wave.hip) of shadow-ray pixel slots
     uint32_t*           qcount;    // QSEG segment counters, QSTRIDE words apart
     size_t              qcap;      // entries per queue segment
     uint64_t*           mt_state;  // [n/64][2][312][64]
     unsigned long long* counters;  // [rays, shadow_rays, samples, draws, primary_hits]
     unsigned long long* wstat;     // per-wave statistics slots (wave_stat_bytes)
+    int64_t             sh_slot0;  // first wstat slot of this part's shadow waves
     unsigned long long* diag;      // optional per-wave timeline (SP_WAVE_DIAG): 4 u64 per wave
 };
 
@@ -31,7 +33,7 @@ constexpr int WF_MAX_LIGHTS = 32; // light mask is one u32 per pixel
 
 size_t     wave_bytes_per_pixel(int n_lights);
 size_t     wave_stat_bytes(int64_t n);
-size_t     wave_queue_bytes(int64_t n);
+size_t     wave_queue_bytes(int64_t n, int n_lights);
 // ev: optional 3 * spp + 3 events recorded around the launches of part 0 (stage timing);
 // aux (may be null): second stream for the overlapped second part, fork/join its events.
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
