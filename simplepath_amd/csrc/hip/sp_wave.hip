@@ -201,7 +201,8 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uin
 }
 
 // Shading: direct_nee's sampling half (Integrator.cpp:287-296).
-__global__ void __launch_bounds__(WF_BLOCK, 3) wf_shade(Scene sc, WaveArgs w, uint32_t sample)
+template <int MINW>
+__global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w, uint32_t sample)
 {
     extern __shared__ uint32_t lds[];
     const int rs_words = 2 << sc.rsqrt_bits;
@@ -498,6 +499,11 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_stats(WaveArgs w, int64_t n_slots
 }
 
 // ---------------------------------------------------------------------------- host side
+static int shade_waves_env()
+{
+    const char* v = std::getenv("SP_SHADE_WAVES");
+    return v ? std::atoi(v) : 4;
+}
 static bool shadow_dyn_env()
 {
     const char* v = std::getenv("SP_SHADOW_DYN"); // opt-in: slower on coherent shadow rays
@@ -574,6 +580,14 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     }
     const uint32_t diag_sample = diag_sample_env();
     const bool     dyn         = shadow_dyn_env();
+    // waves per SIMD requested for the shading kernel (register budget vs spills)
+    void (*shade)(Scene, WaveArgs, uint32_t) = wf_shade<4>;
+    switch (shade_waves_env()) {
+    case 3: shade = wf_shade<3>; break;
+    case 5: shade = wf_shade<5>; break;
+    case 6: shade = wf_shade<6>; break;
+    default: break;
+    }
     unsigned       grid[2], sgrid[2];
     WaveArgs       pd[2];
     for (int k = 0; k < parts; ++k) {
@@ -595,7 +609,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
             hipLaunchKernelGGL(wf_primary, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
             if (k == 0) mark();
             if (parts > 1 && (k == 1 || i > 0)) (void)hipStreamWaitEvent(st, shade_done[1 - k], 0);
-            hipLaunchKernelGGL(wf_shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, pd[k], i);
+            hipLaunchKernelGGL(shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, pd[k], i);
             if (parts > 1) (void)hipEventRecord(shade_done[k], st);
             if (k == 0) mark();
             if (dyn) hipLaunchKernelGGL(wf_shadow_dyn, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
