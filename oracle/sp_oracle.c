@@ -1082,6 +1082,39 @@ typedef struct {
     uint64_t       rays, shadow, samples;
 } Job;
 
+/* MandelbrotIntegrator::integrate_impl + mandel (Integrators/Integrator.cpp:59-105), HSV
+ * to_rgb (math/HSV.h:133, the active #else branch) */
+static C3 integrate_mandelbrot(float px, float py, int W, int H)
+{
+    const float x0 = -2.0f, x1 = 1.0f, y0 = -1.0f, y1 = 1.0f;
+    const float dx = (x1 - x0) / (float)W;
+    const float dy = (y1 - y0) / (float)H;
+    const float cre = x0 + px * dx, cim = y0 + py * dy;
+    float zr = cre, zi = cim;
+    int it = 0;
+    for (; it < 4096; ++it) {
+        if (zr * zr + zi * zi > 4.0f) break;
+        const float nr = zr * zr - zi * zi;
+        const float ni = 2.0f * zr * zi;
+        zr = cre + nr;
+        zi = cim + ni;
+    }
+    const float value = (float)it / (float)4096;
+    const float hue   = fmodf(orc_powf(value * 360.0f, 1.5f), 360.0f) / 360.0f;
+    const float Cc    = value * 1.0f;
+    const int   hp    = (int)floorf(hue * 6.0f);
+    const float X     = (float)((double)Cc * (1.0 - fabs(fmod((double)hp, 2.0) - 1.0)));
+    switch (hp % 6) {
+    case 0: return c3(Cc, X, 0);
+    case 1: return c3(X, Cc, 0);
+    case 2: return c3(0, Cc, X);
+    case 3: return c3(0, X, Cc);
+    case 4: return c3(X, 0, Cc);
+    case 5: return c3(Cc, 0, X);
+    }
+    return c3(0, 0, 0);
+}
+
 static void render_tile(Job* j, int64_t slot)
 {
     const OScene* sc = j->sc;
@@ -1112,6 +1145,7 @@ static void render_tile(Job* j, int64_t slot)
             ray.d = vnormalize(vadd(vadd(fmulv(fx, sc->cam.vx), fmulv(fy, sc->cam.vy)), sc->cam.vz));
             C3 L;
             switch (j->integrator) {
+            case SP_INTEGRATOR_MANDELBROT: L = integrate_mandelbrot(fx, fy, W, H); break;
             case SP_INTEGRATOR_BRUTE_FORCE: L = integrate_bruteforce(&c, ray, 0); break;
             case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE: L = integrate_iterative(&c, ray, 0); break;
             case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: L = integrate_iterative(&c, ray, 1); break;

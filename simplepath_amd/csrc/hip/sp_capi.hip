@@ -641,7 +641,6 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = s->host->integrator;
     if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = SP_INTEGRATOR_DIRECT_LIGHTING; // main.cpp:390
     if (integ < SP_INTEGRATOR_MANDELBROT || integ > SP_INTEGRATOR_WHITTED) return fail(SP_ERR_ARG, "Unknown integrator type");
-    if (integ == SP_INTEGRATOR_MANDELBROT) return fail(SP_ERR_UNSUPPORTED, "mandelbrot integrator is not on the device path yet");
     if ((integ == SP_INTEGRATOR_BRUTE_FORCE || integ == SP_INTEGRATOR_WHITTED) && s->host->max_depth > MAX_RECURSION)
         return fail(SP_ERR_UNSUPPORTED, "recursive integrators support max_depth <= 32");
     int64_t total;

@@ -12,6 +12,7 @@ KernelFn select_kernel(int integ, int variant)
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE:
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: return mega_iterative(integ);
     case SP_INTEGRATOR_ITERATIVE_RRNEE: return mega_rrnee();
+    case SP_INTEGRATOR_MANDELBROT: return mega_mandelbrot();
     default: return mega_direct(variant);
     }
 }

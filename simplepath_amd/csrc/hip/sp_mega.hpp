@@ -71,7 +71,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
                 Ray ray;
                 ray.o = sc.camera.p;
                 ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
-                acc   = cadd(acc, integrate<INTEG>(c, ray)); // image(p) += integrate(...)
+                if constexpr (INTEG == SP_INTEGRATOR_MANDELBROT)
+                    acc = cadd(acc, integrate_mandelbrot(fx, fy, sc.width, sc.height));
+                else
+                    acc = cadd(acc, integrate<INTEG>(c, ray)); // image(p) += integrate(...)
             }
             acc = cdivs(acc, (float)args.spp); // image(p) /= num_pixel_samples
             rays_total += c.rays;
@@ -97,5 +100,6 @@ KernelFn mega_direct(int variant);
 KernelFn mega_iterative(int integ);
 KernelFn mega_rrnee();
 KernelFn mega_recursive(int integ);
+KernelFn mega_mandelbrot();
 
 } // namespace spd

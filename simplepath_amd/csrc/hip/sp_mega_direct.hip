@@ -11,4 +11,5 @@ KernelFn mega_direct(int variant)
     default: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, 2>;
     }
 }
+KernelFn mega_mandelbrot() { return sp_render_kernel<SP_INTEGRATOR_MANDELBROT, 2>; }
 } // namespace spd

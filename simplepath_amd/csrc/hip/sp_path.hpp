@@ -1587,6 +1587,40 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
 }
 
 // ============================================================================ the kernel
+// MandelbrotIntegrator::integrate_impl + mandel (Integrators/Integrator.cpp:59-105) with
+// to_rgb (math/HSV.h:133, the active #else branch).  No scene queries, no sampler draws.
+__device__ __forceinline__ rgb integrate_mandelbrot(float px, float py, int W, int H)
+{
+    const float x0 = -2.0f, x1 = 1.0f, y0 = -1.0f, y1 = 1.0f;
+    const float dx = (x1 - x0) / (float)W;
+    const float dy = (y1 - y0) / (float)H;
+    const float cre = x0 + px * dx, cim = y0 + py * dy;
+    float       zr = cre, zi = cim;
+    int         it = 0;
+    for (; it < 4096; ++it) { // s_max_iterations (Integrator.h:69)
+        if (zr * zr + zi * zi > 4.0f) break;
+        const float nr = zr * zr - zi * zi;
+        const float ni = 2.0f * zr * zi;
+        zr             = cre + nr;
+        zi             = cim + ni;
+    }
+    const float value = (float)it / (float)4096;
+    const float hue   = fmodf(lm_powf(value * 360.0f, 1.5f), 360.0f) / 360.0f; // fmod is exact
+    const float C     = value * 1.0f;
+    const int   hp    = (int)floorf(hue * 6.0f);
+    // std::fmod(int, float) promotes to double: X = C * (1 - |hp mod 2 - 1|) = hp odd ? C : 0
+    const float X = (hp & 1) ? C : 0.0f * C;
+    switch (hp % 6) {
+    case 0: return mkc(C, X, 0);
+    case 1: return mkc(X, C, 0);
+    case 2: return mkc(0, C, X);
+    case 3: return mkc(0, X, C);
+    case 4: return mkc(X, 0, C);
+    case 5: return mkc(C, 0, X);
+    }
+    return mkc(0, 0, 0);
+}
+
 __device__ __forceinline__ uint32_t morton_decode_1(uint32_t a)
 {
     a = a & 0x55555555u;

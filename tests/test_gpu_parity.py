@@ -42,7 +42,7 @@ def test_bunny_direct_lighting_bitexact(scene_dir, pipeline):
 
 
 @pytest.mark.parametrize("integrator", ["direct_lighting", "brute_force", "brute_force_iterative",
-                                        "brute_force_iterative_rr", "iterative_rrnee", "whitted"])
+                                        "brute_force_iterative_rr", "iterative_rrnee", "whitted", "mandelbrot"])
 def test_every_integrator_bitexact(scene_dir, integrator):
     s = load(scene_dir, "material_spheres.sp", 24, 48, bvh=1)
     g, _ = sp.render_tiles(s, integrator, 3)
@@ -131,6 +131,17 @@ def test_wavefront_tile_chunks(scene_dir, monkeypatch):
     assert ast.launches > 3 + 3 * 3
     assert np.array_equal(a, ref)
     assert np.array_equal(b[ids], ref)
+
+
+def test_mandelbrot_full_frame_vs_reference(scene_dir):
+    # the test integrator needs no scene queries: whole 96x64 frame, 2 spp, bit-exact
+    from tests import test_oracle_vs_ref as R
+    s = load(scene_dir, "bunny.sp", 96, 64, bvh=1)
+    g, st = sp.render_tiles(s, "mandelbrot", 2)
+    assert st.rays == 0 and st.rng_draws == 0
+    c, _ = _oracle.render(s, sp.string_to_integrator_type("mandelbrot"), 2, variant="glibc")
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
+    assert g.max() > 0.0
 
 
 def test_wavefront_rejects_other_integrators(scene_dir):

@@ -33,8 +33,6 @@ def test_oracle_libm_variants_bitexact(scene_dir):
 def test_every_integrator_runs(scene_dir):
     s = _scene(scene_dir, "material_spheres.sp", 24, 40)
     for name, val in sp.INTEGRATORS.items():
-        if name == "mandelbrot":
-            continue
         t, st = _oracle.render(s, val, 2, variant="glibc")
         assert np.isfinite(t).all() or name in ("brute_force",), name
         assert st["samples"] == 2 * 24 * 40

@@ -78,7 +78,7 @@ def test_bunny_clipped_tiles_and_order(ref, scene_dir):
 
 
 @pytest.mark.parametrize("integrator", ["direct_lighting", "brute_force", "brute_force_iterative",
-                                        "brute_force_iterative_rr", "iterative_rrnee", "whitted"])
+                                        "brute_force_iterative_rr", "iterative_rrnee", "whitted", "mandelbrot"])
 def test_spheres_every_integrator(ref, scene_dir, integrator):
     path = os.path.join(scene_dir, "material_spheres.sp")
     t = sp.string_to_integrator_type(integrator)
