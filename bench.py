@@ -29,14 +29,26 @@ MT_BYTES_PER_DRAW = 24.0  # 8 B draw read + (2496 B twist read + 2496
 PIXEL_BYTES = 12.0  # one float3 radiance store per pixel
 
 
+# BASELINE.json configs: scene writer, file name, default width / height / spp, data note.
+SCENES = {
+    "bunny": ("write_bunny_scene", "bunny.sp", 1920, 1080, 256,
+              "synthetic (bunny-like PLY generated in-process; scene parameters of scenes/bunny.sp)"),
+    "spheres": ("write_material_spheres_scene", "material_spheres_ibl.sp", 1024, 1024, 64,
+                "synthetic 4096x2048 HDR night map in place of clarens_night_02_4k.pfm; scene parameters of "
+                "scenes/material_spheres.sp"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--scene", default="bunny", choices=sorted(SCENES),
+                    help="bunny = configs[2] (default, the north-star workload); spheres = configs[1]")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--integrator", default="direct_lighting")
     ap.add_argument("--bvh", type=int, default=0, help="0 = SAH, 1 = reference median split")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
@@ -44,7 +56,12 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    sc = SCENES[a.scene]
+    a.width = a.width or sc[2]
+    a.height = a.height or sc[3]
+    a.spp = a.spp or sc[4]
+    return a
 
 
 def main():
@@ -68,11 +85,12 @@ def main():
     from simplepath_amd import scenes
 
     scene_dir = os.path.join(tempfile.gettempdir(), f"sp_bench_{os.getuid()}")
+    writer, fname = SCENES[args.scene][0], SCENES[args.scene][1]
     if rank == 0:
-        path = scenes.write_bunny_scene(scene_dir)
+        getattr(scenes, writer)(scene_dir)
     if dist is not None:
         dist.barrier()
-    path = os.path.join(scene_dir, "bunny.sp")
+    path = os.path.join(scene_dir, fname)
     scene = sp.Scene.from_file(path)
     scene.set_resolution(args.width, args.height)
     scene.upload(device=local, bvh_mode=args.bvh)
@@ -149,8 +167,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (bunny-like PLY generated in-process; scene parameters of scenes/bunny.sp)",
-        "config": {"workload": f"bunny.sp {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
+        "data": SCENES[args.scene][5],
+        "config": {"workload": f"{SCENES[args.scene][1]} {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
                    "width": args.width, "height": args.height, "spp": args.spp, "integrator": args.integrator,
                    "bvh": "sah" if args.bvh == 0 else "reference", "tiles": int(n_tiles),
                    "pipeline": ["auto", "megakernel", "wavefront"][stats[-1].pipeline],
@@ -190,7 +208,8 @@ def roofline_of(stats, pixels, args, kernel_ms):
         try:
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
-            if tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp:
+            if (tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp
+                    and tj.get("scene", "bunny") == args.scene):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 1
+#define SP_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------- */
 enum {
@@ -116,12 +116,25 @@ enum { SP_LIGHT_SPHERE = 0, SP_LIGHT_ENVIRONMENT = 1, SP_LIGHT_IMAGE_ENVIRONMENT
 
 typedef struct sp_light_desc {
     int32_t   kind;
-    int32_t   pad;
+    int32_t   image;           /* SP_LIGHT_IMAGE_ENVIRONMENT: index into sp_scene_desc.env_images, else -1 */
     float     radiance[3];
     sp_affine object_to_world; /* sphere light */
     sp_affine world_to_object;
     sp_linear normal_to_world;
 } sp_light_desc;
+
+/* Image-based environment light (Lights/Light.h:196 ImageBasedEnvironmentLight) as the parser
+ * hands it to the light's constructor (base/FileParser.cpp:366-368): the PFM image (Image/
+ * Image.cpp:78 read_pfm) already multiplied by `radiance`, before the constructor's
+ * modify_image / create_distribution (those run at sp_scene_upload, and in the oracle). */
+typedef struct sp_env_image {
+    int32_t      width, height;
+    const float* pixels;          /* img(x, y) = pixels[(y * width + x) * 3 + c]              */
+    float        max_radiance;    /* std::numeric_limits<float>::max() when not given          */
+    int32_t      reserved;
+    sp_linear    light_to_world;  /* LinearTransformation: rotate/scale attributes             */
+    sp_linear    world_to_light;  /* its inverse (Transformation::get_inverse)                  */
+} sp_env_image;
 
 /* PerspectiveCamera (Cameras/Camera.h:85): the transform built by create_transform. */
 typedef struct sp_camera_desc {
@@ -153,6 +166,9 @@ typedef struct sp_scene_desc {
     int64_t                num_prims;
     const sp_light_desc*   lights;     /* Scene::m_lights order                              */
     const sp_material_desc* materials;
+    const sp_env_image*    env_images; /* referenced by sp_light_desc.image (ABI 2)          */
+    int32_t                num_env_images;
+    int32_t                reserved;
 } sp_scene_desc;
 
 /* ---- render ------------------------------------------------------------------------ */

@@ -18,7 +18,7 @@ OUT="$HERE/_ref"
 mkdir -p "$OUT"
 FLAGS="-std=gnu++20 -O2 -ffp-contract=off -mfma -mavx2 -fPIC -w -I$REF"
 INC="-include optional -include algorithm -include numeric -include sstream -include iomanip -include mutex -include cstring -include limits -include atomic"
-SRCS="Integrators/Integrator.cpp materials/Material.cpp math/Sampling.cpp shapes/Triangle.cpp base/Logger.cpp"
+SRCS="Integrators/Integrator.cpp materials/Material.cpp math/Sampling.cpp shapes/Triangle.cpp base/Logger.cpp Image/Image.cpp"
 pids=()
 for s in $SRCS; do
   o="$OUT/$(basename "$s" .cpp).o"

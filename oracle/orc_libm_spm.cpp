@@ -10,4 +10,5 @@ float orc_logf(float x) { return spm::lm_logf(x); }
 float orc_powf(float x, float y) { return spm::lm_powf(x, y); }
 float orc_erff(float x) { return spm::lm_erff(x); }
 float orc_acosf(float x) { return spm::lm_acosf(x); }
+float orc_atan2f(float y, float x) { return spm::lm_atan2f(y, x); }
 }

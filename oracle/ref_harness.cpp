@@ -2,7 +2,8 @@
 //
 // Renders tiles with the REFERENCE's own code: the scene is assembled from the reference's
 // classes (PerspectiveCamera, OneSampleMaterial / ClearcoatMaterial via create_*_material, Mesh +
-// Triangle, Sphere, Plane, SphereLight, EnvironmentLight, Scene with its ListAccelerator/BVH)
+// Triangle, Sphere, Plane, SphereLight, EnvironmentLight, ImageBasedEnvironmentLight with the
+// reference's read_pfm, Scene with its ListAccelerator/BVH)
 // and every pixel runs main.cpp's render_thread body (main.cpp:86-103) with the reference's
 // samplers and Integrator.  Compiled by oracle/build_ref.sh directly from the sources under
 // /root/reference into oracle/_ref/libsp_ref.so; tests/test_oracle_vs_ref.py checks the C
@@ -242,16 +243,28 @@ std::unique_ptr<Scene> build_scene(const std::string& path, int width, int heigh
                 else if (k == "scale") { Vector3 v{ no_init }; ins >> v; transform *= scale(v); }
             });
             lights.push_back(std::make_shared<SphereLight>(radiance, transform));
-        } else if (b.type == "environment_light") {
-            RGB         radiance = RGB::white();
-            std::string file;
+        } else if (b.type == "environment_light") { // FileParser.cpp:325 parse_environment_light
+            auto                  transform{ LinearTransformation::identity() };
+            RGB                   radiance = RGB::white();
+            auto                  max_radiance{ std::numeric_limits<float>::max() };
+            std::filesystem::path file{};
             parse_attrs(b.body, [&](const std::string& k, std::istream& ins) {
                 if (k == "radiance") ins >> radiance;
-                else if (k == "file") { ins >> file; }
-                else { std::string s; std::getline(ins, s); }
+                else if (k == "max_radiance") ins >> max_radiance;
+                else if (k == "image") ins >> file; // std::filesystem::path >> reads std::quoted
+                else if (k == "rotate") { Vector3 a{ no_init }; Degrees d{ no_init }; ins >> a >> d; transform *= rotate(a, Angle{ d }); }
+                else if (k == "scale") { Vector3 v{ no_init }; ins >> v; transform *= scale(v); }
+                else { std::string r; std::getline(ins, r); }
             });
-            if (!file.empty()) throw std::runtime_error("harness: image environment lights not supported");
-            lights.push_back(std::make_shared<EnvironmentLight>(radiance));
+            if (file.empty()) {
+                lights.push_back(std::make_shared<EnvironmentLight>(radiance));
+            } else {
+                // the reference opens the path relative to the working directory; the harness
+                // resolves it against the scene file's directory
+                auto img = read(file.is_absolute() ? file : base_dir / file);
+                img *= radiance;
+                lights.push_back(std::make_shared<ImageBasedEnvironmentLight>(std::move(img), transform, max_radiance));
+            }
         }
     }
     for (const auto& b : blocks) { // pass 2: clearcoat materials

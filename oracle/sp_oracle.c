@@ -31,6 +31,7 @@ float orc_logf(float);
 float orc_powf(float, float);
 float orc_erff(float);
 float orc_acosf(float);
+float orc_atan2f(float, float);
 
 /* ------------------------------------------------------------------ math (math/*.h) */
 typedef struct { float x, y, z; } V3;
@@ -199,6 +200,7 @@ typedef struct {
     int*                 unbounded_lights;
     OBvh                 lbvh;
     int                  max_depth, rr_depth;
+    struct OEnv*         envs; /* per sp_env_image */
 } OScene;
 
 typedef struct {
@@ -468,15 +470,161 @@ static int scene_intersect(const OScene* sc, const Ray* ray, float tmin, float t
     if (sc->bvh.n_prims && node_intersect(sc, &sc->bvh, 0, ray, tmin, &tmax, out, 0, NULL)) hit = 1;
     return hit;
 }
+/* ------------------------------------------------------------------ image environment light
+ * ImageBasedEnvironmentLight (Lights/Light.h:196): constructor (modify_image :296,
+ * create_distribution :317, math/Distribution1D.h:16, math/Distribution2D.h:10) and its
+ * sample / pdf / intersect_lights (:206-290), in the reference's operation order. */
+typedef struct OEnv {
+    int    w, h, nu, nv;
+    float *rad, *cfunc, *ccdf, *cint, *mfunc, *mcdf;
+    float  mint;
+    Lin    l2w, w2l;
+} OEnv;
+static const float MAX_LESS_THAN_ONE = 0x1.fffffep-1f; /* base/Constants.h:15 */
+static float rel_lum(float r, float g, float b) { return 0.2126f * r + 0.7152f * g + 0.0722f * b; } /* math/RGB.h:224 */
+/* sample_nearest_neighbor(img, s, t, RemapWrap{}, RemapClamp{}) (Image/Image.h:84-117) */
+static size_t env_texel_index(int w, int h, float s, float t)
+{
+    s = fmodf(1.0f + fmodf(s, 1.0f), 1.0f);
+    t = (t < 0.0f) ? 0.0f : ((MAX_LESS_THAN_ONE < t) ? MAX_LESS_THAN_ONE : t);
+    float u = roundf(s * (float)w), v = roundf(t * (float)h);
+    uint32_t x = (uint32_t)u, y = (uint32_t)v;
+    if (x > (uint32_t)(w - 1)) x = (uint32_t)(w - 1);
+    if (y > (uint32_t)(h - 1)) y = (uint32_t)(h - 1);
+    return (size_t)y * (size_t)w + x;
+}
+static C3 env_texel(const OEnv* e, float s, float t)
+{
+    const float* c = &e->rad[env_texel_index(e->w, e->h, s, t) * 3];
+    return c3(c[0], c[1], c[2]);
+}
+/* Distribution1D(f, 0, 1) constructor, including its one-slot-shifted normalisation */
+static void dist1d_build(const float* fin, size_t n, float* func, float* cdf, float* integral)
+{
+    for (size_t i = 0; i < n; ++i) func[i] = fabsf(fin[i]);
+    cdf[0] = 0.0f;
+    for (size_t i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + func[i - 1] * (1.0f - 0.0f) / (float)n;
+    float I = cdf[n];
+    *integral = I;
+    if (I == 0.0f) {
+        for (size_t i = 1; i < n + 1; ++i) cdf[i] = (float)i / (float)n;
+    } else {
+        for (size_t i = 0; i < n; ++i) cdf[i] = cdf[i + 1] / I;
+    }
+}
+static void env_build(const sp_env_image* img, OEnv* e)
+{
+    const float maxr = img->max_radiance;
+    e->w = img->width;
+    e->h = img->height;
+    size_t np = (size_t)e->w * (size_t)e->h;
+    e->rad = (float*)malloc(np * 3 * sizeof(float));
+    memcpy(e->rad, img->pixels, np * 3 * sizeof(float));
+    for (size_t p = 0; p < np; ++p) { /* modify_image */
+        float* c = &e->rad[p * 3];
+        for (int i = 0; i < 3; ++i)
+            if (isinf(c[i])) c[i] = maxr;
+        if (rel_lum(c[0], c[1], c[2]) > maxr) {
+            int mi = (c[0] > c[1]) ? ((c[0] > c[2]) ? 0 : 2) : ((c[1] > c[2]) ? 1 : 2);
+            for (int i = 0; i < 3; ++i) c[i] = c[i] * maxr / c[mi];
+        }
+    }
+    int width = 2 * e->w, height = 2 * e->h; /* create_distribution */
+    float* f = (float*)malloc((size_t)width * height * sizeof(float));
+    for (int v = 0; v < height; ++v) {
+        float vp = ((float)v + 0.5f) / (float)height;
+        float st = orc_sinf(PI_F * ((float)v + 0.5f) / (float)height);
+        for (int u = 0; u < width; ++u) {
+            float up = ((float)u + 0.5f) / (float)width;
+            const float* c = &e->rad[env_texel_index(e->w, e->h, up, vp) * 3];
+            float x = rel_lum(c[0], c[1], c[2]);
+            x *= st;
+            if (isinf(x)) x = maxr;
+            x = (maxr < x) ? maxr : x;
+            f[(size_t)u + (size_t)v * width] = x;
+        }
+    }
+    e->nu = width;
+    e->nv = height;
+    e->cfunc = (float*)malloc((size_t)width * height * sizeof(float));
+    e->ccdf = (float*)malloc((size_t)(width + 1) * height * sizeof(float));
+    e->cint = (float*)malloc((size_t)height * sizeof(float));
+    for (int v = 0; v < height; ++v)
+        dist1d_build(&f[(size_t)v * width], (size_t)width, &e->cfunc[(size_t)v * width], &e->ccdf[(size_t)v * (width + 1)], &e->cint[v]);
+    e->mfunc = (float*)malloc((size_t)height * sizeof(float));
+    e->mcdf = (float*)malloc((size_t)(height + 1) * sizeof(float));
+    dist1d_build(e->cint, (size_t)height, e->mfunc, e->mcdf, &e->mint);
+    e->l2w = from_lin(&img->light_to_world);
+    e->w2l = from_lin(&img->world_to_light);
+    free(f);
+}
+static void env_free(OEnv* e)
+{
+    free(e->rad); free(e->cfunc); free(e->ccdf); free(e->cint); free(e->mfunc); free(e->mcdf);
+}
+/* Distribution1D::get_offset: std::ranges::upper_bound (libstdc++) over cdf[0..n] */
+static size_t dist_offset(const float* cdf, size_t n, float u)
+{
+    size_t first = 0, len = n + 1;
+    while (len > 0) {
+        size_t half = len >> 1, mid = first + half;
+        if (u < cdf[mid]) len = half;
+        else { first = mid + 1; len = len - half - 1; }
+    }
+    if (first == n + 1 || first == n) return n - 1;
+    return first;
+}
+/* Distribution1D::sample_continuous (math/Distribution1D.h:72) */
+static float dist_sample(const float* func, const float* cdf, size_t n, float integral, float u, float* pdf, size_t* off)
+{
+    size_t o = dist_offset(cdf, n, u);
+    *off = o;
+    float du = u - cdf[o];
+    if ((cdf[o + 1] - cdf[o]) > 0) du /= (cdf[o + 1] - cdf[o]);
+    *pdf = (integral > 0) ? func[o] / integral : 0.0f;
+    float x = ((float)o + du) / (float)n;
+    return (1.0f - x) * 0.0f + x * 1.0f; /* sp::lerp(x, m_min, m_max) */
+}
+static float sph_theta(V3 v) { return orc_acosf(v.y < -1.0f ? -1.0f : (1.0f < v.y ? 1.0f : v.y)); } /* math/Sampling.h:82 */
+static float sph_phi(V3 v) /* math/Sampling.h:87 */
+{
+    float p = orc_atan2f(v.z, v.x);
+    return (p < 0.0f) ? (p + 2.0f * PI_F) : p;
+}
+static const float INV_2_PI = 1.0f / (2.0f * 3.14159265358979323846f);
+static const float INV_PI = 0.318309886183790671538f;
+static C3 env_radiance(const OEnv* e, V3 dir) /* intersect_lights_impl (Lights/Light.h:206) */
+{
+    V3 w = vnormalize(lin_vec(e->w2l.vx, e->w2l.vy, e->w2l.vz, dir));
+    return env_texel(e, sph_phi(w) * INV_2_PI, sph_theta(w) * INV_PI);
+}
+/* size_t conversion + std::clamp of Distribution2D::pdf, as x86-64 GCC converts float -> size_t */
+static size_t size_clamp(float x, size_t n)
+{
+    if (x >= 0.0f) return (x >= (float)n) ? n - 1 : (size_t)x;
+    return (x > -1.0f) ? 0 : n - 1;
+}
+static float env_pdf(const OEnv* e, V3 wi) /* pdf_impl (Lights/Light.h:270) */
+{
+    V3 w = lin_vec(e->w2l.vx, e->w2l.vy, e->w2l.vz, wi);
+    float theta = sph_theta(w), phi = sph_phi(w);
+    float st = orc_sinf(theta);
+    if (st == 0.0f) return 0.0f;
+    float p0 = phi * INV_2_PI, p1 = theta * PI_F;
+    size_t iu = size_clamp(p0 * (float)e->nu, (size_t)e->nu), iv = size_clamp(p1 * (float)e->nv, (size_t)e->nv);
+    float dpdf = e->cfunc[iv * (size_t)e->nu + iu] / e->mint;
+    return dpdf / (2.0f * (PI_F * PI_F) * st);
+}
 /* Scene::intersect_lights (base/Scene.h:69) */
 static int scene_intersect_lights(const OScene* sc, const Ray* ray, float tmin, float tmax, float* dist, C3* L)
 {
     int hit = 0;
     for (int i = 0; i < sc->n_unbounded_lights; ++i) {
         const sp_light_desc* l = &sc->d->lights[sc->unbounded_lights[i]];
-        if (!(tmax < INF_DIST)) { /* EnvironmentLight::intersect_lights_impl (Lights/Light.h:242) */
+        if (!(tmax < INF_DIST)) { /* EnvironmentLight / ImageBasedEnvironmentLight::intersect_lights_impl (Lights/Light.h:152, :206) */
             tmax = INF_DIST;
-            *L   = c3(l->radiance[0], l->radiance[1], l->radiance[2]);
+            if (l->kind == SP_LIGHT_IMAGE_ENVIRONMENT) *L = env_radiance(&sc->envs[l->image], ray->d);
+            else *L = c3(l->radiance[0], l->radiance[1], l->radiance[2]);
             hit  = 1;
         }
     }
@@ -858,12 +1006,32 @@ static float sphere_pdf(const sp_light_desc* l, V3 obs) /* shapes/Sphere.h:271 *
     float omc = (s2 < 0.00068523f) ? s2 / 2.0f : 1.0f - cm;
     return 1.0f / (2.0f * PI_F * omc);
 }
-static LS light_sample(const sp_light_desc* l, V3 obs, V3 obs_n, P2 u)
+static LS light_sample(const OScene* sc, const sp_light_desc* l, V3 obs, V3 obs_n, P2 u)
 {
     LS s;
     V3 wi;
     float pdf, maxd;
-    if (l->kind == SP_LIGHT_SPHERE) {
+    s.L = c3(l->radiance[0], l->radiance[1], l->radiance[2]);
+    if (l->kind == SP_LIGHT_IMAGE_ENVIRONMENT) { /* ImageBasedEnvironmentLight::light_sample (Lights/Light.h:243) */
+        const OEnv* e = &sc->envs[l->image];
+        float pdf1, pdf0;
+        size_t v, iu;
+        float d1 = dist_sample(e->mfunc, e->mcdf, (size_t)e->nv, e->mint, u.y, &pdf1, &v);
+        float d0 = dist_sample(&e->cfunc[v * (size_t)e->nu], &e->ccdf[v * (size_t)(e->nu + 1)], (size_t)e->nu, e->cint[v], u.x, &pdf0, &iu);
+        float map_pdf = pdf0 * pdf1;
+        maxd = INF_DIST;
+        if (map_pdf == 0.0f) {
+            pdf = 0.0f;
+            s.L = c3(0, 0, 0);
+            wi = v3(0, 0, 0);
+        } else {
+            float theta = d1 * PI_F, phi = d0 * 2.0f * PI_F;
+            float ct = orc_cosf(theta), st = orc_sinf(theta), sp = orc_sinf(phi), cp = orc_cosf(phi);
+            wi = lin_vec(e->l2w.vx, e->l2w.vy, e->l2w.vz, v3(st * cp, ct, st * sp));
+            pdf = (st == 0.0f) ? 0.0f : map_pdf / (2.0f * (PI_F * PI_F) * st);
+            s.L = env_texel(e, d0, d1);
+        }
+    } else if (l->kind == SP_LIGHT_SPHERE) {
         Aff w2o = from_aff(&l->world_to_object), o2w = from_aff(&l->object_to_world);
         Lin nrm = from_lin(&l->normal_to_world);
         V3 lo = aff_point(&w2o, obs), local;
@@ -884,7 +1052,6 @@ static LS light_sample(const sp_light_desc* l, V3 obs, V3 obs_n, P2 u)
         pdf = UNIFORM_SPHERE_PDF;
         maxd = INF_DIST;
     }
-    s.L = c3(l->radiance[0], l->radiance[1], l->radiance[2]);
     s.pdf = pdf;
     s.tmin = ray_offset(obs_n, wi);
     s.tmax = maxd;
@@ -899,7 +1066,7 @@ static C3 nee_direct(Ctx* c, const Isect* is, V3 wo) /* Integrator.cpp:295-307 *
     const sp_scene_desc* d = c->sc->d;
     C3 L = c3(0, 0, 0);
     for (int li = 0; li < d->info.num_lights; ++li) {
-        LS ls = light_sample(&d->lights[li], is->p, is->n, next2(&c->rng));
+        LS ls = light_sample(c->sc, &d->lights[li], is->p, is->n, next2(&c->rng));
         if (ls.pdf == 0.0f || cblack(ls.L)) continue;
         V3 wi = ls.ray.d;
         C3 f = mat_eval(d, is->material, wo, wi, is->n, &c->rng);
@@ -994,7 +1161,7 @@ static C3 est_direct_mis(Ctx* c, int li, V3 p, V3 n, V3 wo, int mid) /* Integrat
     const sp_scene_desc* d = c->sc->d;
     const sp_light_desc* l = &d->lights[li];
     C3 Lr = c3(0, 0, 0);
-    LS ls = light_sample(l, p, n, next2(&c->rng));
+    LS ls = light_sample(c->sc, l, p, n, next2(&c->rng));
     if (ls.pdf == 0.0f || cblack(ls.L)) return Lr;
     if (scene_any(c, &ls.ray, ls.tmin, ls.tmax)) return Lr;
     V3 wi = ls.ray.d;
@@ -1009,7 +1176,7 @@ static C3 est_direct_mis(Ctx* c, int li, V3 p, V3 n, V3 wo, int mid) /* Integrat
     }
     MS ms = mat_sample(d, mid, wo, n, &c->rng);
     if (ms.pdf == 0.0f || cblack(ms.color)) return Lr;
-    float lp = (l->kind == SP_LIGHT_SPHERE) ? sphere_pdf(l, p) : UNIFORM_SPHERE_PDF;
+    float lp = (l->kind == SP_LIGHT_SPHERE) ? sphere_pdf(l, p) : (l->kind == SP_LIGHT_IMAGE_ENVIRONMENT) ? env_pdf(&c->sc->envs[l->image], ms.dir) : UNIFORM_SPHERE_PDF;
     if (lp == 0.0f) return Lr;
     float inner = ms.pdf + lp;
     float w = (inner == 0.0f) ? 0.0f : ms.pdf / inner;
@@ -1245,6 +1412,9 @@ int orc_render(const sp_scene_desc* d, int integrator, uint32_t spp, const int32
     build_bvh(&sc.lbvh, lprims, first);
     sc.unbounded_lights = lid + first;
     sc.n_unbounded_lights = nl - first;
+    OEnv* envs = (OEnv*)calloc((size_t)d->num_env_images + 1, sizeof(OEnv));
+    for (int i = 0; i < d->num_env_images; ++i) env_build(&d->env_images[i], &envs[i]);
+    sc.envs = envs;
 
     Job j;
     memset(&j, 0, sizeof j);
@@ -1268,6 +1438,8 @@ int orc_render(const sp_scene_desc* d, int integrator, uint32_t spp, const int32
     free(prims);
     free(lprims);
     free(lid);
+    for (int i = 0; i < d->num_env_images; ++i) env_free(&envs[i]);
+    free(envs);
     return 0;
 }
 

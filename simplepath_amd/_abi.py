@@ -49,9 +49,15 @@ class sp_xform_shape(C.Structure):
 
 
 class sp_light_desc(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("radiance", C.c_float * 3),
+    _fields_ = [("kind", C.c_int32), ("image", C.c_int32), ("radiance", C.c_float * 3),
                 ("object_to_world", sp_affine), ("world_to_object", sp_affine),
                 ("normal_to_world", sp_linear)]
+
+
+class sp_env_image(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("pixels", C.POINTER(C.c_float)),
+                ("max_radiance", C.c_float), ("reserved", C.c_int32),
+                ("light_to_world", sp_linear), ("world_to_light", sp_linear)]
 
 
 class sp_camera_desc(C.Structure):
@@ -76,6 +82,7 @@ class sp_scene_desc(C.Structure):
         ("shapes", C.POINTER(sp_xform_shape)),
         ("prim_kind", C.POINTER(C.c_int32)), ("prim_index", C.POINTER(C.c_int32)), ("num_prims", C.c_int64),
         ("lights", C.POINTER(sp_light_desc)), ("materials", C.POINTER(sp_material_desc)),
+        ("env_images", C.POINTER(sp_env_image)), ("num_env_images", C.c_int32), ("reserved", C.c_int32),
     ]
 
 

@@ -501,4 +501,116 @@ SP_HD float lm_acosf(float x)
     return w + w;
 }
 
+// ------------------------------------------------------------------------------------ atanf
+// fdlibm s_atanf.c as built into glibc 2.35 x86-64 libm.so.6 (atanf @0x3e080, no FMA): the
+// branch limits and the order of every float operation follow that disassembly.  Constants are
+// the words it loads (atanhi/atanlo @0x9ebd0.., aT @0x9ec0c..).
+SP_HD float lm_atanf(float x)
+{
+    const uint32_t hx = f2u(x);
+    const uint32_t ix = hx & 0x7fffffffu;
+    const float    one = 1.0f;
+    if (ix > 0x4bffffffu) {                              // |x| >= 2^25, inf, NaN
+        if (ix > 0x7f800000u) return x86_quiet(x);       // x + x
+        if ((int32_t)hx > 0) return u2f(0x3fc90fdau) + u2f(0x33a22168u);
+        return u2f(0xbfc90fdau) - u2f(0x33a22168u);
+    }
+    int   id;
+    float hi = 0.0f, lo = 0.0f;
+    if (ix <= 0x3edfffffu) {                             // |x| < 0.4375
+        if (ix <= 0x30ffffffu) return x;                 // |x| < 2^-29 (huge + x > one)
+        id = -1;
+    } else {
+        const float ax = abs_f(x);
+        if (ix > 0x3f97ffffu) {
+            if (ix > 0x401bffffu) {                      // 2.4375 <= |x| < 2^25
+                id = 3; hi = u2f(0x3fc90fdau); lo = u2f(0x33a22168u);
+                x  = -1.0f / ax;
+            } else {                                     // 1.1875 <= |x| < 2.4375
+                id = 2; hi = u2f(0x3f7b985eu); lo = u2f(0x33140fb4u);
+                x  = (ax - 1.5f) / (ax * 1.5f + one);
+            }
+        } else if (ix > 0x3f2fffffu) {                   // 11/16 <= |x| < 19/16
+            id = 1; hi = u2f(0x3f490fdau); lo = u2f(0x33222168u);
+            x  = (ax - one) / (ax + one);
+        } else {                                         // 7/16 <= |x| < 11/16
+            id = 0; hi = u2f(0x3eed6338u); lo = u2f(0x31ac3769u);
+            x  = ((ax + ax) - one) / (ax + 2.0f);
+        }
+    }
+    const float z  = x * x;
+    const float w  = z * z;
+    float       s1 = u2f(0x3c8569d7u) * w + u2f(0x3d4bda59u);
+    s1             = s1 * w + u2f(0x3d886b35u);
+    s1             = s1 * w + u2f(0x3dba2e6eu);
+    s1             = s1 * w + u2f(0x3e124925u);
+    s1             = s1 * w + u2f(0x3eaaaaabu);
+    s1             = s1 * z;
+    float s2       = u2f(0xbd15a221u) * w - u2f(0x3d6ef16bu);
+    s2             = s2 * w - u2f(0x3d9d8795u);
+    s2             = s2 * w - u2f(0x3de38e38u);
+    s2             = s2 * w - u2f(0x3e4ccccdu);
+    s2             = s2 * w;
+    const float sx = (s1 + s2) * x;
+    if (id < 0) return x - sx;
+    const float r = hi - ((sx - lo) - x);
+    return ((int32_t)hx < 0) ? -r : r;
+}
+
+// ------------------------------------------------------------------------------------ atan2f
+// fdlibm e_atan2f.c (__atan2f_finite @0x38be0 in the same libm; the atan2f wrapper only sets
+// errno).  y first, x second, like std::atan2.
+SP_HD float lm_atan2f(float y, float x)
+{
+    const uint32_t hx = f2u(x), hy = f2u(y);
+    const uint32_t ix = hx & 0x7fffffffu, iy = hy & 0x7fffffffu;
+    const float    tiny   = u2f(0x0da24260u);
+    const float    pi     = u2f(0x40490fdbu);
+    const float    pi_o_2 = u2f(0x3fc90fdbu);
+    const float    pi_o_4 = u2f(0x3f490fdbu);
+    if (ix > 0x7f800000u || iy > 0x7f800000u) return is_nan_bits(x) ? x86_quiet(x) : x86_quiet(y); // x + y
+    if (hx == 0x3f800000u) return lm_atanf(y);
+    const int m = (int)(((int32_t)hx >> 30) & 2) | (int)(hy >> 31);
+    if (iy == 0) {
+        if (m == 2) return tiny + pi;
+        if (m == 3) return u2f(0xc0490fdbu) - tiny;
+        return y;
+    }
+    if (ix == 0) return ((int32_t)hy < 0) ? u2f(0xbfc90fdbu) - tiny : tiny + pi_o_2;
+    if (ix == 0x7f800000u) {
+        if (iy == 0x7f800000u) {
+            if (m == 2) return 3.0f * pi_o_4 + tiny;
+            if (m == 3) return -3.0f * pi_o_4 - tiny;
+            if (m == 1) return u2f(0xbf490fdbu) - tiny;
+            return tiny + pi_o_4;
+        }
+        if (m == 2) return tiny + pi;
+        if (m == 3) return u2f(0xc0490fdbu) - tiny;
+        return (m == 1) ? -0.0f : 0.0f;
+    }
+    if (iy == 0x7f800000u) return ((int32_t)hy < 0) ? u2f(0xbfc90fdbu) - tiny : tiny + pi_o_2;
+    const int32_t d = (int32_t)iy - (int32_t)ix;
+    float         z;
+    if (d > 0x1e7fffff) z = pi_o_2 - u2f(0x333bbd2eu);                  // |y/x| > 2^60
+    else if ((int32_t)hx < 0 && (d >> 23) < -60) z = 0.0f;               // |y|/x < -2^60
+    else z = lm_atanf(abs_f(y / x));
+    if (m == 0) return z;
+    if (m == 1) return u2f(f2u(z) ^ 0x80000000u);
+    if (m == 2) return pi - (u2f(0x33bbbd2eu) + z);
+    return (z + u2f(0x33bbbd2eu)) - pi;
+}
+
+// std::fmod(f, 1.0f) (glibc fmodf: exact).  For |f| < 2^23 the fraction f - trunc(f) is exact;
+// the result carries the sign of f; inf/NaN give NaN.
+SP_HD float fmod1(float f)
+{
+    const float a = abs_f(f);
+    if (a < 8388608.0f) return copysign_f(f - __builtin_truncf(f), f);
+    if (is_nan_bits(f)) return x86_quiet(f);
+    if (!(a <= 3.40282347e38f)) return x86_default_nan();
+    return copysign_f(0.0f, f);
+}
+// std::round(float): half away from zero (glibc roundf).
+SP_HD float round_f(float f) { return __builtin_roundf(f); }
+
 } // namespace spm

@@ -205,6 +205,7 @@ struct DevBuf {
 struct sp_scene {
     std::unique_ptr<sph::Scene> host;
     sp_scene_desc               desc{};
+    std::vector<sp_env_image>   env_descs; // desc.env_images
     // device residency
     int                  device   = -1;
     int                  bvh_mode = -1;
@@ -309,8 +310,23 @@ void fill_desc(sp_scene* s)
     d.prim_index   = h.prim_index.empty() ? nullptr : h.prim_index.data();
     d.num_prims    = static_cast<int64_t>(h.prim_kind.size());
     d.lights       = h.lights.empty() ? nullptr : h.lights.data();
-    static std::vector<sp_material_desc> dummy;
-    (void)dummy;
+    s->env_descs.clear();
+    for (const auto& e : h.env_images) {
+        sp_env_image x{};
+        x.width        = e.width;
+        x.height       = e.height;
+        x.pixels       = e.pixels.data();
+        x.max_radiance = e.max_radiance;
+        put(x.light_to_world.vx, e.light_to_world.vx);
+        put(x.light_to_world.vy, e.light_to_world.vy);
+        put(x.light_to_world.vz, e.light_to_world.vz);
+        put(x.world_to_light.vx, e.world_to_light.vx);
+        put(x.world_to_light.vy, e.world_to_light.vy);
+        put(x.world_to_light.vz, e.world_to_light.vz);
+        s->env_descs.push_back(x);
+    }
+    d.env_images     = s->env_descs.empty() ? nullptr : s->env_descs.data();
+    d.num_env_images = static_cast<int32_t>(s->env_descs.size());
 }
 
 std::vector<sp_material_desc> material_descs(const sph::Scene& h)
@@ -552,6 +568,7 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     for (auto& l : h.lights) {
         spd::Light x{};
         x.kind     = l.kind;
+        x.image    = l.kind == SP_LIGHT_IMAGE_ENVIRONMENT ? l.image : -1;
         x.radiance = spm::mkc(l.radiance[0], l.radiance[1], l.radiance[2]);
         x.o2w      = from_desc(l.object_to_world);
         x.w2o      = from_desc(l.world_to_object);
@@ -606,6 +623,27 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     d.n_light_nodes = (int)lnodes.size();
     up(lnodes, &d.light_nodes);
     up(light_slot, &d.light_slot);
+    // image environment lights: the constructor's tables (sp_envmap.cpp), then the EnvMap records
+    std::vector<spd::EnvMap> envs;
+    for (const auto& e : h.env_images) {
+        const sph::EnvMap m = sph::build_env_map(e);
+        spd::EnvMap       x{};
+        x.l2w = e.light_to_world;
+        x.w2l = e.world_to_light;
+        x.w = m.w; x.h = m.h; x.nu = m.nu; x.nv = m.nv;
+        std::vector<float4> rad((size_t)m.w * m.h);
+        for (size_t i = 0; i < rad.size(); ++i) rad[i] = make_float4(m.radiance[3 * i], m.radiance[3 * i + 1], m.radiance[3 * i + 2], 0.0f);
+        up(rad, &x.radiance);
+        up(m.cond_func, &x.cond_func);
+        up(m.cond_cdf, &x.cond_cdf);
+        up(m.cond_int, &x.cond_int);
+        up(m.marg_func, &x.marg_func);
+        up(m.marg_cdf, &x.marg_cdf);
+        x.marg_int = m.marg_int;
+        envs.push_back(x);
+    }
+    d.envs = nullptr;
+    up(envs, &d.envs);
     up(mats, &d.materials);
     up(rc.entries, &d.rsqrt_entries);
     if (rc2 != SP_OK) return rc2;

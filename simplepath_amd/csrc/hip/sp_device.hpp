@@ -43,10 +43,24 @@ struct Shape { // sphere / plane
 };
 
 struct Light {
-    int32_t kind, pad;
+    int32_t kind, image; // image: index into Scene::envs for SP_LIGHT_IMAGE_ENVIRONMENT
     rgb     radiance;
     aff     o2w, w2o;
     lin     nrm;
+};
+
+// ImageBasedEnvironmentLight (Lights/Light.h:196) after its constructor: clamped radiance image
+// and the Distribution2D tables (sp_host.hpp EnvMap), read with per-lane binary searches.
+struct EnvMap {
+    lin             l2w, w2l;
+    int32_t         w, h, nu, nv;
+    const float4*   radiance;  // w * h, {r, g, b, 0}
+    const float*    cond_func; // nv * nu
+    const float*    cond_cdf;  // nv * (nu + 1)
+    const float*    cond_int;  // nv
+    const float*    marg_func; // nv
+    const float*    marg_cdf;  // nv + 1
+    float           marg_int;
 };
 
 struct Material {
@@ -87,6 +101,7 @@ struct Scene {
     int             n_light_nodes;
     const Node*     light_nodes;
     const uint32_t* light_slot; // slot -> light index
+    const EnvMap*   envs;       // image environment lights (Light::image)
 
     const Material* materials;
 

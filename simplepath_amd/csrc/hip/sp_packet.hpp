@@ -168,6 +168,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights_w(const Scene& sc, co
     LightHit lh;
     lh.hit = false;
     lh.t   = tmax;
+    lh.env = -1;
     if (on) {
         for (int i = 0; i < sc.n_unbounded_lights; ++i) {
             const Light& l = sc.lights[sc.unbounded_lights[i]];
@@ -175,6 +176,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights_w(const Scene& sc, co
                 lh.hit = true;
                 lh.t   = k_infinite;
                 lh.L   = l.radiance;
+                lh.env = (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) ? l.image : -1;
             }
         }
     }
@@ -200,6 +202,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights_w(const Scene& sc, co
                         lh.hit = true;
                         lh.t   = t;
                         lh.L   = l.radiance;
+                        lh.env = -1;
                     }
                 }
             } else {

@@ -586,7 +586,7 @@ __device__ __forceinline__ Light uload_light(const Light* p)
 {
     Light l;
     l.kind     = (int32_t)uload_u32(&p->kind);
-    l.pad      = 0;
+    l.image    = (int32_t)uload_u32(reinterpret_cast<const uint32_t*>(&p->image));
     const f3 r = uload_f3(reinterpret_cast<const f3*>(&p->radiance));
     l.radiance = mkc(r.x, r.y, r.z);
     l.o2w      = uload_aff(&p->o2w);
@@ -687,12 +687,127 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
     return false;
 }
 
+// ------------------------------------------------------------------------------ image environment light
+// ImageBasedEnvironmentLight (Lights/Light.h:196) on the device.  The tables are the ones its
+// constructor builds (sp_envmap.cpp); the lookups below restate Distribution1D/2D sampling and
+// the nearest-neighbour texel fetch with the reference's operation order.
+
+// Distribution1D::get_offset (math/Distribution1D.h:130): libstdc++ ranges::upper_bound over the
+// n + 1 cdf entries, step for step (the last entry is the integral, not 1, so the array is not
+// sorted and only this exact search reproduces the reference's offsets).
+__device__ __forceinline__ int dist_offset(const float* cdf, int n, float u)
+{
+    int first = 0, len = n + 1;
+    while (len > 0) {
+        const int half = len >> 1;
+        const int mid  = first + half;
+        if (u < cdf[mid]) {
+            len = half;
+        } else {
+            first = mid + 1;
+            len   = len - half - 1;
+        }
+    }
+    return (first >= n) ? n - 1 : first; // it == end() || it == prev(end())
+}
+// Distribution1D::sample_continuous (math/Distribution1D.h:72) on [0, 1]
+__device__ __forceinline__ float dist_sample(const float* func, const float* cdf, int n, float integral, float u, float& pdf, int& off)
+{
+    off            = dist_offset(cdf, n, u);
+    const float c0 = cdf[off], c1 = cdf[off + 1];
+    float       du = u - c0;
+    if ((c1 - c0) > 0.0f) du /= (c1 - c0);
+    pdf           = (integral > 0.0f) ? func[off] / integral : 0.0f;
+    const float x = (static_cast<float>(off) + du) / static_cast<float>(n);
+    return (1.0f - x) * 0.0f + x * 1.0f; // lerp(x, m_min, m_max)
+}
+// static_cast<std::size_t>(x) clamped to [0, n - 1] as x86-64 GCC converts (negative <= -1 and
+// NaN wrap to huge values, which the clamp maps to n - 1).
+__device__ __forceinline__ int size_clamp(float x, int n)
+{
+    if (x >= 0.0f) return (x >= static_cast<float>(n)) ? n - 1 : static_cast<int>(x);
+    return (x > -1.0f) ? 0 : n - 1;
+}
+// sample_nearest_neighbor(img, s, t, RemapWrap, RemapClamp) (Image/Image.h:99)
+__device__ __forceinline__ rgb env_texel(const EnvMap& e, float s, float t)
+{
+    s                = fmod1(1.0f + fmod1(s));
+    t                = std_clamp(t, 0.0f, 0x1.fffffep-1f);
+    const float    u = round_f(s * static_cast<float>(e.w));
+    const float    v = round_f(t * static_cast<float>(e.h));
+    const uint32_t x = min(static_cast<uint32_t>(u), static_cast<uint32_t>(e.w - 1));
+    const uint32_t y = min(static_cast<uint32_t>(v), static_cast<uint32_t>(e.h - 1));
+    const float4   c = e.radiance[(size_t)y * (uint32_t)e.w + x];
+    return mkc(c.x, c.y, c.z);
+}
+// spherical_theta / spherical_phi (math/Sampling.h:82-91)
+__device__ __forceinline__ float spherical_theta(f3 v) { return lm_acosf(std_clamp(v.y, -1.0f, 1.0f)); }
+__device__ __forceinline__ float spherical_phi(f3 v)
+{
+    const float p = lm_atan2f(v.z, v.x);
+    return (p < 0.0f) ? (p + 2.0f * k_pi) : p;
+}
+constexpr float k_inv_2_pi = 1.0f / (2.0f * k_pi);
+// ImageBasedEnvironmentLight::intersect_lights_impl radiance (Lights/Light.h:216)
+__device__ __forceinline__ rgb env_radiance(const EnvMap& e, f3 dir, const Rsq& q)
+{
+    const f3 w = normalize(xfm_vector(e.w2l, dir), q);
+    return env_texel(e, spherical_phi(w) * k_inv_2_pi, spherical_theta(w) * k_inv_pi);
+}
+struct EnvSample {
+    rgb   L;
+    float pdf;
+    f3    wi;
+};
+// ImageBasedEnvironmentLight::light_sample (Lights/Light.h:243)
+__device__ __forceinline__ EnvSample env_sample(const EnvMap& e, P2 u)
+{
+    EnvSample s;
+    float     pdf1, pdf0;
+    int       v, iu;
+    const float d1 = dist_sample(e.marg_func, e.marg_cdf, e.nv, e.marg_int, u.y, pdf1, v);
+    const float d0 = dist_sample(e.cond_func + (size_t)v * e.nu, e.cond_cdf + (size_t)v * (e.nu + 1), e.nu, e.cond_int[v], u.x, pdf0, iu);
+    const float map_pdf = pdf0 * pdf1;
+    if (map_pdf == 0.0f) {
+        s.L   = mkc(0, 0, 0);
+        s.pdf = 0.0f;
+        s.wi  = mk(0, 0, 0);
+        return s;
+    }
+    const float theta     = d1 * k_pi;
+    const float phi       = d0 * 2.0f * k_pi;
+    const float cos_theta = lm_cosf(theta);
+    const float sin_theta = lm_sinf(theta);
+    const float sin_phi   = lm_sinf(phi);
+    const float cos_phi   = lm_cosf(phi);
+    s.wi  = xfm_vector(e.l2w, mk(sin_theta * cos_phi, cos_theta, sin_theta * sin_phi));
+    s.pdf = (sin_theta == 0.0f) ? 0.0f : map_pdf / (2.0f * (k_pi * k_pi) * sin_theta);
+    s.L   = env_texel(e, d0, d1);
+    return s;
+}
+// ImageBasedEnvironmentLight::pdf_impl (Lights/Light.h:270); note the reference passes
+// theta * pi (not theta / pi) as the second coordinate to Distribution2D::pdf.
+__device__ __forceinline__ float env_pdf(const EnvMap& e, f3 wi)
+{
+    const f3    w         = xfm_vector(e.w2l, wi);
+    const float theta     = spherical_theta(w);
+    const float phi       = spherical_phi(w);
+    const float sin_theta = lm_sinf(theta);
+    if (sin_theta == 0.0f) return 0.0f;
+    const int iu = size_clamp(phi * k_inv_2_pi * static_cast<float>(e.nu), e.nu);
+    const int iv = size_clamp(theta * k_pi * static_cast<float>(e.nv), e.nv);
+    return (e.cond_func[(size_t)iv * e.nu + iu] / e.marg_int) / (2.0f * (k_pi * k_pi) * sin_theta);
+}
+
 // ------------------------------------------------------------------------------ lights
 struct LightHit {
-    bool  hit;
-    float t;
-    rgb   L;
+    bool    hit;
+    float   t;
+    rgb     L;   // radiance of the light hit (constant lights)
+    int32_t env; // >= 0: an image environment light won; its radiance depends on the direction
 };
+// LightIntersection::L of a hit (light_hit_L evaluates an image light lazily: the integrators
+// only read L when no geometry is in front of the light).
 
 // Scene::intersect_lights (base/Scene.h:69): ListAccelerator{environment..., BVH(sphere lights)}
 __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
@@ -700,13 +815,15 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
     LightHit lh;
     lh.hit = false;
     lh.t   = tmax;
+    lh.env = -1;
     for (int i = 0; i < sc.n_unbounded_lights; ++i) {
         const Light l = uload_light(sc.lights + uload_u32(sc.unbounded_lights + i));
-        // EnvironmentLight::intersect_lights_impl (Lights/Light.h:242)
+        // EnvironmentLight / ImageBasedEnvironmentLight::intersect_lights_impl (Lights/Light.h:152, :206)
         if (!(lh.t < k_infinite)) {
             lh.hit = true;
             lh.t   = k_infinite;
             lh.L   = l.radiance;
+            lh.env = (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) ? l.image : -1;
         }
     }
     if (sc.n_light_nodes == 0) return lh;
@@ -722,6 +839,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
                 lh.hit = true;
                 lh.t   = t;
                 lh.L   = mkc(r.x, r.y, r.z);
+                lh.env = -1;
             }
         }
         return lh;
@@ -742,6 +860,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
                         lh.hit = true;
                         lh.t   = t;
                         lh.L   = l.radiance;
+                        lh.env = -1;
                     }
                 }
             } else {
@@ -758,6 +877,11 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
         test_box = true;
     }
     return lh;
+}
+
+__device__ __forceinline__ rgb light_hit_L(const Scene& sc, const LightHit& lh, f3 dir, const Rsq& q)
+{
+    return (lh.env >= 0) ? env_radiance(sc.envs[lh.env], dir, q) : lh.L;
 }
 
 __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
@@ -1287,12 +1411,13 @@ __device__ __forceinline__ float sphere_pdf(const Light& l, f3 observer_world)
     return 1.0f / (2.0f * k_pi * omc);
 }
 
-// Light::sample (Lights/Light.h:145) for SphereLight / EnvironmentLight
-__device__ __forceinline__ LSample light_sample(const Light& l, f3 obs, f3 obs_n, P2 u, const Rsq& q)
+// Light::sample (Lights/Light.h:145) for SphereLight / EnvironmentLight / ImageBasedEnvironmentLight
+__device__ __forceinline__ LSample light_sample(const Scene& sc, const Light& l, f3 obs, f3 obs_n, P2 u, const Rsq& q)
 {
     LSample s;
     f3      wi;
     float   pdf, max_dist;
+    s.L = l.radiance;
     if (l.kind == SP_LIGHT_SPHERE) {
         // Sphere::sample(observer, u) (shapes/Sphere.h:245)
         const f3 lo = xfm_point(l.w2o, obs);
@@ -1311,13 +1436,18 @@ __device__ __forceinline__ LSample light_sample(const Light& l, f3 obs, f3 obs_n
         wi                 = normalize(to_sample, q);
         pdf                = sphere_pdf(l, obs);
         max_dist           = length(to_sample) - ray_offset(sn_w, neg(wi));
+    } else if (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) {
+        const EnvSample es = env_sample(sc.envs[l.image], u);
+        wi                 = es.wi;
+        pdf                = es.pdf;
+        s.L                = es.L;
+        max_dist           = k_infinite;
     } else {
         // EnvironmentLight::light_sample (Lights/Light.h:265)
         wi       = sample_uniform_sphere(u);
         pdf      = k_uniform_sphere_pdf;
         max_dist = k_infinite;
     }
-    s.L     = l.radiance;
     s.pdf   = pdf;
     s.tmin  = ray_offset(obs_n, wi);
     s.tmax  = max_dist;
@@ -1325,9 +1455,12 @@ __device__ __forceinline__ LSample light_sample(const Light& l, f3 obs, f3 obs_n
     s.ray.d = wi;
     return s;
 }
-__device__ __forceinline__ float light_pdf(const Light& l, f3 obs, f3 /*wi*/)
+// Light::pdf (Lights/Light.h:54)
+__device__ __forceinline__ float light_pdf(const Scene& sc, const Light& l, f3 obs, f3 wi)
 {
-    return (l.kind == SP_LIGHT_SPHERE) ? sphere_pdf(l, obs) : k_uniform_sphere_pdf;
+    if (l.kind == SP_LIGHT_SPHERE) return sphere_pdf(l, obs);
+    if (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) return env_pdf(sc.envs[l.image], wi);
+    return k_uniform_sphere_pdf;
 }
 
 // ============================================================================ integrators
@@ -1371,7 +1504,7 @@ __device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
     rgb L = mkc(0, 0, 0);
     for (int li = 0; li < c.sc.n_lights; ++li) {
         const Light   l  = uload_light(c.sc.lights + li);
-        const LSample ls = light_sample(l, is.p, is.n, next2D(c.rng), c.q);
+        const LSample ls = light_sample(c.sc, l, is.p, is.n, next2D(c.rng), c.q);
         if (ls.pdf == 0.0f || cblack(ls.L)) continue;
         const f3  wi = ls.ray.d;
         const rgb f  = material_eval(c.sc, is.material, wo, wi, is.n, c.rng, c.q);
@@ -1389,7 +1522,7 @@ __device__ __forceinline__ rgb integrate_direct(Ctx& c, Ray ray)
     if (qr.geom) {
         L = direct_nee(c, qr.is, neg(ray.d));
     } else if (qr.lh.hit) {
-        L = cadd(L, cmul(mkc(1, 1, 1), qr.lh.L));
+        L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(c.sc, qr.lh, ray.d, c.q)));
     }
     return L;
 }
@@ -1426,7 +1559,7 @@ __device__ __forceinline__ rgb integrate_iterative(Ctx& c, Ray ray)
             tmin  = ray_offset(cosine);
             tmax  = k_infinite;
         } else if (qr.lh.hit) {
-            L = cadd(L, cmul(throughput, qr.lh.L));
+            L = cadd(L, cmul(throughput, light_hit_L(c.sc, qr.lh, ray.d, c.q)));
             break;
         } else {
             break;
@@ -1462,7 +1595,7 @@ __device__ __forceinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
             ray.d       = s.dir;
             ++depth;
         } else if (qr.lh.hit) {
-            Lend = qr.lh.L;
+            Lend = light_hit_L(c.sc, qr.lh, ray.d, c.q);
             break;
         } else {
             Lend = mkc(0, 0, 0);
@@ -1498,7 +1631,7 @@ __device__ __forceinline__ rgb integrate_whitted(Ctx& c, Ray ray)
                 }
             }
         } else if (qr.lh.hit) {
-            L = cadd(L, cmul(mkc(1, 1, 1), qr.lh.L));
+            L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(c.sc, qr.lh, ray.d, c.q)));
         }
         Lv[depth] = L;
         if (!more) break;
@@ -1513,7 +1646,7 @@ __device__ __forceinline__ rgb integrate_whitted(Ctx& c, Ray ray)
 __device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p, f3 n, f3 wo, int mid)
 {
     rgb           Lr = mkc(0, 0, 0);
-    const LSample ls = light_sample(l, p, n, next2D(c.rng), c.q);
+    const LSample ls = light_sample(c.sc, l, p, n, next2D(c.rng), c.q);
     if (ls.pdf == 0.0f || cblack(ls.L)) return Lr;
     if (occluded(c, ls.ray, ls.tmin, ls.tmax)) return Lr;
     const f3  wi = ls.ray.d;
@@ -1527,7 +1660,7 @@ __device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p,
     }
     const MSample ms = material_sample(c.sc, mid, wo, n, c.rng, c.q);
     if (ms.pdf == 0.0f || cblack(ms.color)) return Lr;
-    const float lp = light_pdf(l, p, ms.dir);
+    const float lp = light_pdf(c.sc, l, p, ms.dir);
     if (lp == 0.0f) return Lr;
     const float w = balance(ms.pdf, ms.pdf + lp);
     Ray         mr;
@@ -1538,7 +1671,7 @@ __device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p,
     const LightHit lh = scene_intersect_lights(c.sc, mr, mmin, k_infinite, c.st);
     if (lh.hit) {
         if (!occluded(c, mr, mmin, k_infinite))
-            Lr = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, lh.L), abs_f(dot(ms.dir, n))), w), ms.pdf));
+            Lr = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, light_hit_L(c.sc, lh, mr.d, c.q)), abs_f(dot(ms.dir, n))), w), ms.pdf));
     }
     return Lr;
 }
@@ -1577,7 +1710,7 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
             tmin  = ray_offset(cosine);
             tmax  = k_infinite;
         } else if (qr.lh.hit) {
-            L = cadd(L, cmul(throughput, qr.lh.L));
+            L = cadd(L, cmul(throughput, light_hit_L(c.sc, qr.lh, ray.d, c.q)));
             break;
         } else {
             break;

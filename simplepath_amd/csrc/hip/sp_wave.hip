@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uin
                 hrec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
                 hits = 1;
             } else if (lh.hit) {
-                const rgb L = cadd(mkc(0, 0, 0), cmul(mkc(1, 1, 1), lh.L));
+                const rgb L = cadd(mkc(0, 0, 0), cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, q)));
                 w.acc[p]           = w.acc[p] + L.r;
                 w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
                 w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
             const f3    wo  = neg(ray.d);
             for (int li = 0; li < sc.n_lights; ++li) {
                 const Light   l  = uload_light(sc.lights + li);
-                const LSample ls = light_sample(l, is.p, is.n, next2D(rng), q);
+                const LSample ls = light_sample(sc, l, is.p, is.n, next2D(rng), q);
                 if (ls.pdf == 0.0f || cblack(ls.L)) continue;
                 const f3  wi = ls.ray.d;
                 const rgb f  = material_eval(sc, is.material, wo, wi, is.n, rng, q);

@@ -58,6 +58,32 @@ struct Mesh {
     std::vector<uint32_t> indices;
 };
 
+// ImageBasedEnvironmentLight constructor input (base/FileParser.cpp:366-368).
+struct EnvImage {
+    int                width = 0, height = 0;
+    std::vector<float> pixels; // img(x, y) at (y * width + x) * 3, already * radiance
+    float              max_radiance = 3.40282347e38f;
+    lin                light_to_world{}, world_to_light{};
+};
+
+// What the ImageBasedEnvironmentLight constructor derives (Lights/Light.h:196-330): the clamped
+// radiance image (modify_image) and the Distribution2D over a 2x-resolution luminance x
+// sin(theta) image (create_distribution, math/Distribution2D.h, math/Distribution1D.h),
+// restated with the same float operation order.
+struct EnvMap {
+    int                w = 0, h = 0;          // radiance image
+    std::vector<float> radiance;              // 3 per pixel, modify_image applied
+    int                nu = 0, nv = 0;        // distribution grid (2w x 2h)
+    std::vector<float> cond_func;             // nv x nu   Distribution1D::m_function (abs)
+    std::vector<float> cond_cdf;              // nv x (nu + 1) m_cdf as the constructor leaves it
+    std::vector<float> cond_int;              // nv        m_function_integral
+    std::vector<float> marg_func, marg_cdf;   // nv, nv + 1
+    float              marg_int = 0.0f;
+};
+EnvMap build_env_map(const EnvImage& img);
+// Image/Image.cpp:78 read_pfm: img(x, y), rows stored bottom-up in the file.
+void read_pfm(const std::string& path, int& w, int& h, std::vector<float>& pixels);
+
 struct Scene {
     int         image_width  = 512; // FileParser defaults (base/FileParser.cpp:256-259)
     int         image_height = 512;
@@ -75,6 +101,7 @@ struct Scene {
     std::vector<std::string>    material_names;
     std::vector<sp_xform_shape> shapes;
     std::vector<sp_light_desc>  lights;
+    std::vector<EnvImage>       env_images; // sp_light_desc.image indexes this
     // triangles of all meshes, concatenated (global vertex numbering)
     std::vector<f3>       vertices;
     std::vector<f3>       normals;

@@ -699,25 +699,45 @@ private:
             return true;
         });
     }
+    // FileParser::parse_environment_light (base/FileParser.cpp:325)
     void environment_light(const std::string& body)
     {
         rgb         radiance = mkc(1, 1, 1);
         std::string image;
-        AffXf       xf{ aff_identity(), aff_identity() };
+        float       max_radiance = 3.40282347e38f; // std::numeric_limits<float>::max()
+        AffXf       xf{ aff_identity(), aff_identity() }; // LinearTransformation: p stays unused
         attributes(body, "environment light", [&](const std::string& w, Cursor& c) {
             if (w == "radiance") { f3 v = c.get_vec3(); radiance = mkc(v.x, v.y, v.z); }
-            else if (w == "max_radiance") c.get_float();
+            else if (w == "max_radiance") max_radiance = c.get_float();
             else if (w == "image") image = c.get_path();
             else if (w == "rotate") { f3 a = c.get_vec3(); float d = c.get_float(); append_rotate(xf, a, d); }
             else if (w == "scale") append_scale(xf, c.get_vec3());
             else return false;
             return true;
         });
-        if (!image.empty())
-            throw SpError(SP_ERR_UNSUPPORTED, "image-based environment light is a later row (Lights/Light.h:286)");
         sp_light_desc l{};
-        l.kind        = SP_LIGHT_ENVIRONMENT;
+        l.image       = -1;
         l.radiance[0] = radiance.r; l.radiance[1] = radiance.g; l.radiance[2] = radiance.b;
+        if (image.empty()) {
+            l.kind = SP_LIGHT_ENVIRONMENT;
+        } else {
+            // `read(filename)` then `img *= radiance` (FileParser.cpp:366-367).  The reference
+            // resolves the path against the working directory; here the scene file's directory
+            // is tried first (resolve()).
+            EnvImage e;
+            read_pfm(resolve(m_base, image), e.width, e.height, e.pixels);
+            for (size_t i = 0; i < e.pixels.size(); i += 3) {
+                e.pixels[i] *= radiance.r;
+                e.pixels[i + 1] *= radiance.g;
+                e.pixels[i + 2] *= radiance.b;
+            }
+            e.max_radiance   = max_radiance;
+            e.light_to_world = lin{ xf.fwd.vx, xf.fwd.vy, xf.fwd.vz };
+            e.world_to_light = lin{ xf.inv.vx, xf.inv.vy, xf.inv.vz };
+            l.kind  = SP_LIGHT_IMAGE_ENVIRONMENT;
+            l.image = (int32_t)m_scene->env_images.size();
+            m_scene->env_images.push_back(std::move(e));
+        }
         m_scene->lights.push_back(l);
     }
     void material_lambertian(const std::string& body)
@@ -821,6 +841,7 @@ private:
         });
         sp_light_desc l{};
         l.kind = SP_LIGHT_SPHERE;
+        l.image = -1;
         l.radiance[0] = radiance.r; l.radiance[1] = radiance.g; l.radiance[2] = radiance.b;
         to_desc(xf.fwd, l.object_to_world);
         to_desc(xf.inv, l.world_to_object);

@@ -153,7 +153,7 @@ def write_bunny_scene(directory: str) -> str:
 
 
 # scenes/material_spheres.sp with its image environment light replaced by a uniform
-# environment_light (the HDR map is not available; image lights are a later row).
+# environment_light plus a sphere light: a cheaper variant used by most parity tests.
 def spheres_sp(env_radiance: str = "1.0 1.0 1.0", with_sphere_light: bool = True) -> str:
     s = """version: 1
 
@@ -261,4 +261,79 @@ def write_spheres_scene(directory: str, with_sphere_light: bool = True) -> str:
     path = os.path.join(directory, "material_spheres.sp")
     with open(path, "w") as fh:
         fh.write(spheres_sp(with_sphere_light=with_sphere_light))
+    return path
+
+
+# ---------------------------------------------------------------- image environment light
+def night_sky_image(width: int = 4096, height: int = 2048, seed: int = 2) -> np.ndarray:
+    """Synthetic stand-in for clarens_night_02_4k.pfm (not in the reference repository): a
+    lat-long HDR night scene, img[y, x] in Image(x, y) order (y = 0 is theta = 0, straight up).
+    Dim sky gradient, a bright moon, a row of street lamps near the horizon whose cores exceed
+    the scene's max_radiance (100), a dark ground, and a few adversarial texels: +inf (handled by
+    ImageBasedEnvironmentLight::modify_image), negative values (Distribution1D takes abs) and
+    fully black rows (zero-integral conditional distributions)."""
+    rng = np.random.default_rng(seed)
+    v = (np.arange(height) + 0.5) / height
+    u = (np.arange(width) + 0.5) / width
+    theta = (np.pi * v)[:, None]
+    phi = (2.0 * np.pi * u)[None, :]
+    up = np.cos(theta)
+    sky = np.where(up > 0, 0.02 + 0.08 * (1.0 - up) ** 3, 0.004 + 0.002 * np.sin(7 * phi) ** 2)
+    img = np.stack([sky * 0.6, sky * 0.7, sky * 1.2], axis=-1) * np.ones((height, width, 1))
+    # stars
+    n_stars = width * height // 4000
+    sy = rng.integers(0, height // 2, n_stars)
+    sx = rng.integers(0, width, n_stars)
+    img[sy, sx] += rng.uniform(0.5, 4.0, (n_stars, 1))
+    # moon: a disc of radiance ~ 40
+    d = np.array([np.sin(0.7) * np.cos(2.0), np.cos(0.7), np.sin(0.7) * np.sin(2.0)])
+    dirs = np.stack([np.sin(theta) * np.cos(phi), np.cos(theta) * np.ones_like(phi), np.sin(theta) * np.sin(phi)], -1)
+    cosang = dirs @ d
+    img[cosang > np.cos(0.03)] = (40.0, 38.0, 30.0)
+    # street lamps just above the horizon: cores far above max_radiance, halos around them
+    for k in range(9):
+        lc = np.array([np.sin(1.45) * np.cos(0.3 + 0.7 * k), np.cos(1.45), np.sin(1.45) * np.sin(0.3 + 0.7 * k)])
+        c = dirs @ lc
+        img += (c > np.cos(0.05))[..., None] * np.array([6.0, 4.0, 1.5])
+        img[c > np.cos(0.008)] = (900.0 + 50 * k, 600.0, 250.0)
+    img = img.astype(np.float32)
+    img[height // 3, width // 5] = (np.inf, 1.0, 1.0)
+    img[height // 2 + 3, width // 7] = (-0.5, -0.25, 0.1)
+    img[height - 1, :] = 0.0
+    img[height - 2, :] = 0.0
+    return img
+
+
+def write_pfm(path: str, img: np.ndarray) -> None:
+    """Image/Image.cpp:40 write_pfm layout: little-endian, rows bottom-up (img[y, x] = img(x, y))."""
+    h, w, _ = img.shape
+    with open(path, "wb") as fh:
+        fh.write(f"PF\n{w} {h}\n-1\n".encode())
+        fh.write(np.ascontiguousarray(img[::-1].astype("<f4")).tobytes())
+
+
+def material_spheres_sp(image: str = "clarens_night_02_4k.pfm") -> str:
+    """scenes/material_spheres.sp verbatim: analytic spheres lit only by the image-based
+    environment light (rotate 45 deg about y, max_radiance 100)."""
+    s = spheres_sp(with_sphere_light=False)
+    head = s[: s.index("environment_light {")]
+    return head + """environment_light {
+    rotate: 0.0 1.0 0.0 45.0
+    radiance: 1.0 1.0 1.0
+    max_radiance: 100
+    image: "%s"
+}
+""" % image
+
+
+def write_material_spheres_scene(directory: str, width: int = 4096, height: int = 2048,
+                                 image: str = "clarens_night_02_4k.pfm",
+                                 name: str = "material_spheres_ibl.sp") -> str:
+    os.makedirs(directory, exist_ok=True)
+    pfm = os.path.join(directory, image)
+    if not os.path.exists(pfm):
+        write_pfm(pfm, night_sky_image(width, height))
+    path = os.path.join(directory, name)
+    with open(path, "w") as fh:
+        fh.write(material_spheres_sp(image))
     return path

@@ -18,4 +18,6 @@ def scene_dir(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("scenes"))
     scenes.write_bunny_scene(d)
     scenes.write_spheres_scene(d)
+    # image-lit material_spheres.sp with a small synthetic HDR map (the 4k map is the bench's)
+    scenes.write_material_spheres_scene(d, 96, 48, image="night_96x48.pfm")
     return d

@@ -91,7 +91,18 @@ def test_vs_glibc_oracle_bitexact(scene_dir, integrator):
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
 
 
-@pytest.mark.parametrize("scene,bvh", [("bunny.sp", 0), ("material_spheres.sp", 1)])
+@pytest.mark.parametrize("integrator", ["direct_lighting", "brute_force_iterative_rr", "iterative_rrnee", "whitted",
+                                        "brute_force"])
+def test_image_environment_light_bitexact(scene_dir, integrator):
+    # ImageBasedEnvironmentLight: Distribution2D sampling, MIS pdf, escaping-ray lookups
+    s = load(scene_dir, "material_spheres_ibl.sp", 24, 48, bvh=1)
+    g, gst = sp.render_tiles(s, integrator, 4)
+    c, cst = _oracle.render(s, sp.string_to_integrator_type(integrator), 4, variant="glibc")
+    assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), (integrator, rel_l2(g, c))
+
+
+@pytest.mark.parametrize("scene,bvh", [("bunny.sp", 0), ("material_spheres.sp", 1), ("material_spheres_ibl.sp", 0)])
 def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
     # the two device pipelines run the same floating-point sequence per pixel
     s = load(scene_dir, scene, 72, 40, bvh=bvh)
@@ -153,7 +164,9 @@ def test_wavefront_rejects_other_integrators(scene_dir):
 @pytest.mark.parametrize("scene,w,h,integrator,spp", [("bunny.sp", 64, 40, "direct_lighting", 4),
                                                       ("bunny.sp", 32, 24, "iterative_rrnee", 2),
                                                       ("material_spheres.sp", 24, 48, "whitted", 3),
-                                                      ("material_spheres.sp", 24, 48, "brute_force_iterative_rr", 3)])
+                                                      ("material_spheres.sp", 24, 48, "brute_force_iterative_rr", 3),
+                                                      ("material_spheres_ibl.sp", 24, 48, "direct_lighting", 4),
+                                                      ("material_spheres_ibl.sp", 24, 48, "iterative_rrnee", 3)])
 def test_vs_reference_build_bitexact(scene_dir, scene, w, h, integrator, spp):
     # the HIP path against the reference's own code (oracle/_ref, built from its sources)
     from tests import test_oracle_vs_ref as R

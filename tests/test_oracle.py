@@ -23,11 +23,12 @@ def test_oracle_deterministic_and_thread_independent(scene_dir):
 
 def test_oracle_libm_variants_bitexact(scene_dir):
     # the product libm (sp_libm.h) is an exact glibc emulation: both oracle builds agree bit for bit
-    s = _scene(scene_dir, "bunny.sp", 48, 32)
-    for integ in (6, 5):
-        a, _ = _oracle.render(s, integ, 4, variant="glibc")
-        b, _ = _oracle.render(s, integ, 4, variant="spm")
-        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), integ
+    for name, w, h in (("bunny.sp", 48, 32), ("material_spheres_ibl.sp", 24, 48)):
+        s = _scene(scene_dir, name, w, h)
+        for integ in (6, 5):
+            a, _ = _oracle.render(s, integ, 4, variant="glibc")
+            b, _ = _oracle.render(s, integ, 4, variant="spm")
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (name, integ)
 
 
 def test_every_integrator_runs(scene_dir):

@@ -94,3 +94,18 @@ def test_bunny_multibounce(ref, scene_dir):
     r = ref_render(ref, path, 32, 24, 5, 2, ids)
     o = oracle_render(path, 32, 24, 5, 2, ids)
     assert same(r, o)
+
+
+@pytest.mark.parametrize("integrator", ["direct_lighting", "brute_force_iterative_rr", "iterative_rrnee", "whitted",
+                                        "brute_force"])
+def test_image_environment_light(ref, scene_dir, integrator):
+    """scenes/material_spheres.sp with its ImageBasedEnvironmentLight (synthetic HDR map with
+    clamped, infinite, negative and black texels): light sampling through Distribution2D,
+    the light pdf of the MIS integrator, and radiance lookups of escaping rays."""
+    path = os.path.join(scene_dir, "material_spheres_ibl.sp")
+    t = sp.string_to_integrator_type(integrator)
+    ids = np.arange(sp.TileScheduler(24, 48).get_num_tiles(), dtype=np.int32)
+    r = ref_render(ref, path, 24, 48, t, 4, ids)
+    o = oracle_render(path, 24, 48, t, 4, ids)
+    assert same(r, o), (integrator, float(np.abs(r - o).max()), int(np.sum(r != o)))
+    assert r.max() > 0.0

@@ -1,6 +1,6 @@
 // Exhaustive bit-exactness check of spm::lm_* (simplepath_amd/csrc/common/sp_libm.h) against the
 // host glibc float libm.  Usage: libm_exhaustive <func> [stride] [threads]
-//   func: sinf cosf expf logf erff acosf powf
+//   func: sinf cosf expf logf erff acosf atanf fmod1 roundf powf atan2f
 // Prints "<func> checked=<n> mismatches=<m>" and up to 8 examples.
 #include "../simplepath_amd/csrc/common/sp_libm.h"
 #include <atomic>
@@ -30,7 +30,34 @@ int main(int argc, char** argv)
             std::printf("%s\n", buf);
         }
     };
-    if (fn == "powf") {
+    if (fn == "atan2f") {  // pairs: random bits, unit-vector components (the reference's use), specials
+        std::vector<std::thread> th;
+        for (int t = 0; t < nth; ++t)
+            th.emplace_back([&, t] {
+                std::mt19937_64 rng(777 + t);
+                uint64_t c = 0, b = 0;
+                const uint64_t n = (stride > 1 ? 4000000ull : 100000000ull) / nth;
+                const float sp[] = {0.0f, -0.0f, 1.0f, -1.0f, INFINITY, -INFINITY, NAN, 1e-38f, -1e-38f, 1e38f, -1e38f, 1e-45f};
+                for (uint64_t i = 0; i < n; ++i) {
+                    float x, y;
+                    const int mode = i % 4;
+                    if (mode == 0) { y = flt((uint32_t)rng()); x = flt((uint32_t)rng()); }
+                    else if (mode == 1) {
+                        y = (float)((double)(rng() >> 11) * 0x1.0p-53 * 2.0 - 1.0);
+                        x = (float)((double)(rng() >> 11) * 0x1.0p-53 * 2.0 - 1.0);
+                    } else if (mode == 2) {
+                        y = sp[rng() % 12]; x = ((rng() & 1) ? sp[rng() % 12] : flt((uint32_t)rng()));
+                        if (rng() & 1) std::swap(x, y);
+                    } else { const float a = flt((uint32_t)rng()); y = a * (float)(int)(rng() % 7 - 3); x = a * (float)(int)(rng() % 7 - 3) + flt((uint32_t)rng() & 0x807fffffu); }
+                    const float want = atan2f(y, x), got = spm::lm_atan2f(y, x);
+                    ++c;
+                    if (bits(want) != bits(got)) { ++b; report(y, x, got, want); }
+                }
+                checked += c;
+                bad += b;
+            });
+        for (auto& x : th) x.join();
+    } else if (fn == "powf") {
         std::vector<std::thread> th;
         for (int t = 0; t < nth; ++t)
             th.emplace_back([&, t] {
@@ -63,6 +90,9 @@ int main(int argc, char** argv)
         else if (fn == "logf") { ref = logf; emu = [](float x) { return spm::lm_logf(x); }; }
         else if (fn == "erff") { ref = erff; emu = [](float x) { return spm::lm_erff(x); }; }
         else if (fn == "acosf") { ref = acosf; emu = [](float x) { return spm::lm_acosf(x); }; }
+        else if (fn == "atanf") { ref = atanf; emu = [](float x) { return spm::lm_atanf(x); }; }
+        else if (fn == "fmod1") { ref = [](float x) { return fmodf(x, 1.0f); }; emu = [](float x) { return spm::fmod1(x); }; }
+        else if (fn == "roundf") { ref = roundf; emu = [](float x) { return spm::round_f(x); }; }
         else { std::printf("unknown %s\n", fn.c_str()); return 2; }
         std::vector<std::thread> th;
         const uint64_t total = 1ull << 32;
