@@ -29,13 +29,19 @@ MT_BYTES_PER_DRAW = 24.0  # 8 B draw read + (2496 B twist read + 2496
 PIXEL_BYTES = 12.0  # one float3 radiance store per pixel
 
 
-# BASELINE.json configs: scene writer, file name, default width / height / spp, data note.
+# BASELINE.json configs: scene writer, file name, default width / height / spp / integrator, data note.
 SCENES = {
-    "bunny": ("write_bunny_scene", "bunny.sp", 1920, 1080, 256,
-              "synthetic (bunny-like PLY generated in-process; scene parameters of scenes/bunny.sp)"),
-    "spheres": ("write_material_spheres_scene", "material_spheres_ibl.sp", 1024, 1024, 64,
-                "synthetic 4096x2048 HDR night map in place of clarens_night_02_4k.pfm; scene parameters of "
-                "scenes/material_spheres.sp"),
+    "bunny": dict(writer="write_bunny_scene", file="bunny.sp", w=1920, h=1080, spp=256, integrator="direct_lighting",
+                  data="synthetic (bunny-like PLY generated in-process; scene parameters of scenes/bunny.sp)"),
+    "spheres": dict(writer="write_material_spheres_scene", file="material_spheres_ibl.sp", w=1024, h=1024, spp=64,
+                    integrator="direct_lighting",
+                    data="synthetic 4096x2048 HDR night map in place of clarens_night_02_4k.pfm; scene parameters of "
+                         "scenes/material_spheres.sp"),
+    "lucy": dict(writer="write_lucy_scene", file="lucy.sp", w=1920, h=1080, spp=256, integrator="direct_lighting",
+                 data="synthetic 28.05M-triangle lucy-like PLY generated in-process; scene parameters of scenes/lucy.sp"),
+    "elf": dict(writer="write_elf_scene", file="elf.sp", w=4096, h=4096, spp=1024, integrator="iterative_rrnee",
+                data="synthetic 1.0M-triangle figure as binary STL generated in-process; scene parameters of "
+                     "scenes/elf.sp + max_depth 16"),
 }
 
 
@@ -45,11 +51,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="bunny", choices=sorted(SCENES),
-                    help="bunny = configs[2] (default, the north-star workload); spheres = configs[1]")
+                    help="bunny = configs[2] (default, the north-star workload); spheres = configs[1]; "
+                         "lucy = configs[3]; elf = configs[4]")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--integrator", default="direct_lighting")
+    ap.add_argument("--integrator", default=None)
     ap.add_argument("--bvh", type=int, default=0, help="0 = SAH, 1 = reference median split")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -58,9 +65,10 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
     a = ap.parse_args()
     sc = SCENES[a.scene]
-    a.width = a.width or sc[2]
-    a.height = a.height or sc[3]
-    a.spp = a.spp or sc[4]
+    a.width = a.width or sc["w"]
+    a.height = a.height or sc["h"]
+    a.spp = a.spp or sc["spp"]
+    a.integrator = a.integrator or sc["integrator"]
     return a
 
 
@@ -85,7 +93,7 @@ def main():
     from simplepath_amd import scenes
 
     scene_dir = os.path.join(tempfile.gettempdir(), f"sp_bench_{os.getuid()}")
-    writer, fname = SCENES[args.scene][0], SCENES[args.scene][1]
+    writer, fname = SCENES[args.scene]["writer"], SCENES[args.scene]["file"]
     if rank == 0:
         getattr(scenes, writer)(scene_dir)
     if dist is not None:
@@ -167,8 +175,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": SCENES[args.scene][5],
-        "config": {"workload": f"{SCENES[args.scene][1]} {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
+        "data": SCENES[args.scene]["data"],
+        "config": {"workload": f"{fname} {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
                    "width": args.width, "height": args.height, "spp": args.spp, "integrator": args.integrator,
                    "bvh": "sah" if args.bvh == 0 else "reference", "tiles": int(n_tiles),
                    "pipeline": ["auto", "megakernel", "wavefront"][stats[-1].pipeline],

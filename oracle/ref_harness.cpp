@@ -173,6 +173,69 @@ std::shared_ptr<Mesh> read_ply_mesh(const std::filesystem::path& path, const Aff
     return std::make_shared<Mesh>(Mesh{ std::move(indices), std::move(vertices), std::move(vertex_normals), object_to_world });
 }
 
+// STLReader restatement (base/STLReader.cpp:46 read_binary_stl, which g++ 11 cannot compile
+// here): std::map<Point3, index> vertex welding, the file's face normal unless is_zero (then the
+// edge cross product), zero-area faces skipped after their indices were pushed, vertex normals
+// = normalize(sum of face normals).
+std::shared_ptr<Mesh> read_stl_mesh(const std::filesystem::path& path, const AffineTransformation& object_to_world)
+{
+    std::ifstream ins(path, std::ios::binary);
+    if (!ins) throw std::runtime_error("cannot open " + path.string());
+    std::array<char, 80> header;
+    ins.read(header.data(), 80);
+    std::uint32_t num_triangles = 0;
+    ins.read(reinterpret_cast<char*>(&num_triangles), 4);
+    std::map<Point3, std::size_t>        index_of;
+    std::vector<Point3>                  vertices;
+    std::vector<std::size_t>             vertex_indices;
+    std::vector<std::array<unsigned, 3>> faces;
+    std::vector<Normal3>                 face_normals;
+    for (std::uint32_t i = 0; i < num_triangles; ++i) {
+        float nx, ny, nz;
+        ins.read(reinterpret_cast<char*>(&nx), 4);
+        ins.read(reinterpret_cast<char*>(&ny), 4);
+        ins.read(reinterpret_cast<char*>(&nz), 4);
+        Normal3                 fn{ nx, ny, nz };
+        std::array<unsigned, 3> fv{};
+        for (std::size_t j = 0; j < 3; ++j) {
+            float x, y, z;
+            ins.read(reinterpret_cast<char*>(&x), 4);
+            ins.read(reinterpret_cast<char*>(&y), 4);
+            ins.read(reinterpret_cast<char*>(&z), 4);
+            const Point3 v{ x, y, z };
+            std::size_t  index;
+            if (const auto it = index_of.find(v); it != index_of.end()) {
+                index = it->second;
+            } else {
+                index = index_of.size();
+                index_of.emplace(v, index);
+            }
+            if (index >= vertices.size()) vertices.push_back(v);
+            fv[j] = static_cast<unsigned>(index);
+            vertex_indices.push_back(index);
+        }
+        std::uint16_t attributes;
+        ins.read(reinterpret_cast<char*>(&attributes), 2);
+        if (is_zero(fn)) {
+            const Vector3 edge0 = vertices.at(fv[1]) - vertices.at(fv[0]);
+            const Vector3 edge1 = vertices.at(fv[2]) - vertices.at(fv[0]);
+            fn                  = Normal3{ cross(edge0, edge1) };
+        }
+        if (is_zero(fn)) continue;
+        fn = normalize(fn);
+        faces.push_back(fv);
+        face_normals.push_back(fn);
+    }
+    std::vector vertex_normals(vertices.size(), Normal3{ 0.0f, 0.0f, 0.0f });
+    for (size_t k = 0; k < faces.size(); ++k)
+        for (int i = 0; i < 3; ++i) vertex_normals.at(faces[k][i]) += face_normals[k];
+    for (auto& n : vertex_normals) {
+        if (n != Normal3{ 0.0f, 0.0f, 0.0f }) n = normalize(n);
+        else n = Normal3{ 0.0f, 1.0f, 0.0f };
+    }
+    return std::make_shared<Mesh>(Mesh{ std::move(vertex_indices), std::move(vertices), std::move(vertex_normals), object_to_world });
+}
+
 template <typename F>
 void parse_attrs(const std::string& body, F&& f)
 {
@@ -295,7 +358,8 @@ std::unique_ptr<Scene> build_scene(const std::string& path, int width, int heigh
             else if (k == "scale") { Vector3 v{ no_init }; ins >> v; transform *= scale(v); }
         });
         if (b.type == "mesh") {
-            auto mesh = read_ply_mesh(base_dir / file, transform);
+            const auto fp   = base_dir / file;
+            auto       mesh = fp.extension() == ".stl" ? read_stl_mesh(fp, transform) : read_ply_mesh(fp, transform);
             for (std::size_t i = 0; i < mesh->get_num_triangles(); ++i)
                 geometry.push_back(std::make_shared<GeometricPrimitive>(std::make_shared<Triangle>(mesh, i), material));
         } else if (b.type == "plane") {

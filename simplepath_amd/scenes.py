@@ -337,3 +337,231 @@ def write_material_spheres_scene(directory: str, width: int = 4096, height: int 
     with open(path, "w") as fh:
         fh.write(material_spheres_sp(image))
     return path
+
+
+# ---------------------------------------------------------------- lucy.sp / elf.sp
+def cube_sphere(n: int):
+    """Welded cube-sphere grid: unit directions (V, 3) float64 and triangles (12 n^2, 3) int32,
+    outward winding.  Vertices are welded by their integer lattice position on the cube surface
+    (cheap at tens of millions of triangles)."""
+    keys, quads = [], []
+    i, j = np.meshgrid(np.arange(n + 1), np.arange(n + 1), indexing="ij")
+    i, j = i.ravel(), j.ravel()
+    qi, qj = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    q00 = (qi * (n + 1) + qj).ravel()
+    base = 0
+    lat = []
+    for axis in range(3):
+        for sign in (1, -1):
+            a1, a2 = (axis + 1) % 3, (axis + 2) % 3
+            c = np.empty((i.size, 3), dtype=np.int64)
+            c[:, axis] = n if sign > 0 else 0
+            c[:, a1] = i
+            c[:, a2] = j
+            lat.append(c)
+            v00, v10, v01, v11 = q00 + base, q00 + base + (n + 1), q00 + base + 1, q00 + base + n + 2
+            if sign > 0:
+                quads.append(np.stack([v00, v10, v11, v01], -1))
+            else:
+                quads.append(np.stack([v00, v01, v11, v10], -1))
+            base += i.size
+    lat = np.concatenate(lat)
+    key = (lat[:, 0] * (n + 1) + lat[:, 1]) * (n + 1) + lat[:, 2]
+    uniq, first, inverse = np.unique(key, return_index=True, return_inverse=True)
+    lat = lat[first]
+    t = np.tan((lat / n * 2.0 - 1.0) * (np.pi / 4))  # equal-angle grid
+    d = t / np.linalg.norm(t, axis=1, keepdims=True)
+    q = inverse.reshape(-1)[np.concatenate(quads)]
+    f = np.concatenate([q[:, [0, 1, 2]], q[:, [0, 2, 3]]]).astype(np.int32)
+    return d, f
+
+
+def _lobes(d: np.ndarray, lobes, ripples) -> np.ndarray:
+    r = np.ones(d.shape[0])
+    for c, w, a in lobes:
+        c = np.asarray(c, dtype=np.float64)
+        c = c / np.linalg.norm(c)
+        r += a * np.exp(-np.sum((d - c) ** 2, axis=1) / w)
+    for amp, fx, fy, fz in ripples:
+        r += amp * np.sin(fx * d[:, 0] + 0.3) * np.sin(fy * d[:, 1] + 0.7) * np.sin(fz * d[:, 2] + 1.1)
+    return r
+
+
+def lucy_mesh(n: int = 1529):
+    """Stand-in for the Stanford lucy.ply (14.0 M vertices, 28.06 M triangles; not in the
+    reference repository): n = 1529 gives 14.03 M vertices / 28.05 M triangles.  A tall winged
+    figure (radial lobes for head, wings, arms and robe) with drapery-like ripples at several
+    frequencies, so the BVH is deep and boxes overlap like a scanned statue's.  Coordinates are
+    in lucy.ply's frame: lucy.sp rotates it by -90 deg about x, stands it on the plane at
+    y = -605.893 and frames it from (690.756, 500, -2000)."""
+    d, f = cube_sphere(n)
+    lobes = [((0.0, 0.0, 1.0), 0.05, 0.35),      # head (up = +z in the file frame)
+             ((0.9, 0.3, 0.6), 0.10, 0.9),       # wing
+             ((-0.9, 0.3, 0.6), 0.10, 0.9),      # wing
+             ((0.6, -0.6, 0.1), 0.06, 0.35),     # arm
+             ((-0.5, -0.7, 0.3), 0.06, 0.3),     # arm
+             ((0.0, 0.0, -1.0), 0.4, 0.45)]      # robe
+    ripples = [(0.02, 37.0, 29.0, 41.0), (0.008, 131.0, 97.0, 113.0), (0.003, 401.0, 367.0, 389.0)]
+    p = d * _lobes(d, lobes, ripples)[:, None] * np.array([0.45, 0.3, 1.0])
+    lo, hi = p.min(axis=0), p.max(axis=0)
+    box_lo = np.array([690.756 - 420.0, -192.627 - 260.0, -605.893])
+    box_hi = np.array([690.756 + 420.0, -192.627 + 260.0, -605.893 + 1610.0])
+    p = box_lo + (p - lo) / (hi - lo) * (box_hi - box_lo)
+    return p.astype(np.float32), f
+
+
+def elf_mesh(n: int = 290):
+    """Stand-in for stl_files/elf/nude-body.stl (not in the reference repository): a standing
+    figure, 1.0 M triangles at n = 290, feet on elf.sp's plane (y = -42.7188), centred on its
+    camera axis (x = -1.795, y = -0.034) at z = 13.84."""
+    d, f = cube_sphere(n)
+    lobes = [((0.0, 1.0, 0.0), 0.04, 0.3),       # head
+             ((0.7, 0.45, 0.0), 0.05, 0.5),      # arms
+             ((-0.7, 0.45, 0.0), 0.05, 0.5),
+             ((0.25, -1.0, 0.0), 0.03, 0.45),    # legs
+             ((-0.25, -1.0, 0.0), 0.03, 0.45)]
+    ripples = [(0.01, 23.0, 31.0, 19.0), (0.004, 89.0, 71.0, 97.0)]
+    p = d * _lobes(d, lobes, ripples)[:, None] * np.array([0.35, 1.0, 0.2])
+    lo, hi = p.min(axis=0), p.max(axis=0)
+    box_lo = np.array([-1.79536 - 18.0, -42.7188, 13.8378 - 8.0])
+    box_hi = np.array([-1.79536 + 18.0, 42.7, 13.8378 + 8.0])
+    p = box_lo + (p - lo) / (hi - lo) * (box_hi - box_lo)
+    return p.astype(np.float32), f
+
+
+def write_stl(path: str, verts: np.ndarray, faces: np.ndarray) -> None:
+    """Binary STL (base/STLReader.cpp:46 layout): 80-byte header, count, then per triangle the
+    unit face normal, three vertices and a 2-byte attribute count."""
+    tri = verts[faces].astype(np.float32)
+    nrm = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]).astype(np.float64)
+    ln = np.linalg.norm(nrm, axis=1, keepdims=True)
+    nrm = np.where(ln > 0, nrm / np.where(ln > 0, ln, 1.0), 0.0).astype(np.float32)
+    rec = np.zeros(faces.shape[0], dtype=[("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")])
+    rec["n"], rec["v"] = nrm, tri
+    with open(path, "wb") as fh:
+        fh.write(b"synthetic stand-in for nude-body.stl".ljust(80, b" "))
+        fh.write(np.uint32(faces.shape[0]).tobytes())
+        fh.write(rec.tobytes())
+
+
+_FIGURE_MATERIALS = """material_glossy {
+    name: "material_glossy_base"
+    diffuse: 0.7 0.7 0.7
+    ior: 1.3
+    roughness: 0.75
+}
+
+material_glossy {
+    name: "material_glossy_plane"
+    diffuse: 0.4 0.1 0.1
+    ior: 1.8
+    roughness: 0.01
+}
+
+material_clearcoat {
+    name: "material_glossy_clearcoat"
+    base: "material_glossy_base"
+    ior: 1.5
+    color: 1.0 1.0 1.0
+}
+"""
+
+
+def lucy_sp(ply_rel: str) -> str:
+    """scenes/lucy.sp of the reference (mesh path pointing at the synthetic PLY)."""
+    return f"""version: 1
+
+scene_parameters {{
+    output_file_name: "image.pfm"
+    width: 1350
+    height: 2000
+}}
+
+perspective_camera {{
+    origin: 690.756 500.0 -2000.0
+    look_at: 690.756 200.0 192.627
+    fov: 45
+}}
+
+{_FIGURE_MATERIALS}
+mesh {{
+    file: "{ply_rel}"
+    rotate: 1.0 0.0 0.0 -90.0
+    material: "material_glossy_clearcoat"
+}}
+
+plane {{
+    material: "material_glossy_plane"
+    translate: 0.0 -605.893 0.0
+}}
+
+environment_light {{
+    rotate: 0.0 1.0 0.0 45.0
+    radiance: 1.0 1.0 1.3
+}}
+"""
+
+
+def elf_sp(stl_rel: str, max_depth: int | None = None) -> str:
+    """scenes/elf.sp of the reference; `max_depth` adds a scene_parameters max_depth (the
+    BASELINE config renders it with max-depth 16).  The reference file writes the camera's
+    look_at as "-1.79536, -0.0338669, 13.8378": under its parser (operator>> on floats) the comma
+    fails the stream, so y becomes 0, z is left uninitialised (undefined) and the rest of the
+    camera block is skipped.  The intended coordinates are written here instead."""
+    md = "" if max_depth is None else f"\n    max_depth: {max_depth}"
+    return f"""version: 1
+
+scene_parameters {{
+    output_file_name: "image.pfm"
+    width: 1350
+    height: 2000{md}
+}}
+
+perspective_camera {{
+    origin: -1.79536 -0.0338669 130.0
+    look_at: -1.79536 -0.0338669 13.8378
+    fov: 45
+}}
+
+{_FIGURE_MATERIALS}
+mesh {{
+    file: "{stl_rel}"
+    material: "material_glossy_clearcoat"
+}}
+
+plane {{
+    material: "material_glossy_plane"
+    translate: 0.0 -42.7188 0.0
+}}
+
+environment_light {{
+    rotate: 0.0 1.0 0.0 45.0
+    radiance: 0.75 0.75 0.75
+}}
+"""
+
+
+def _write_once(path: str, writer) -> None:
+    if not os.path.exists(path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tmp = path + ".tmp%d" % os.getpid()
+        writer(tmp)
+        os.replace(tmp, path)
+
+
+def write_lucy_scene(directory: str, n: int = 1529, name: str = "lucy.sp") -> str:
+    rel = os.path.join("ply_files", f"lucy_{n}.ply")
+    _write_once(os.path.join(directory, rel), lambda p: write_ply(p, *lucy_mesh(n)))
+    path = os.path.join(directory, name)
+    with open(path, "w") as fh:
+        fh.write(lucy_sp(rel))
+    return path
+
+
+def write_elf_scene(directory: str, n: int = 290, max_depth: int | None = 16, name: str = "elf.sp") -> str:
+    rel = os.path.join("stl_files", "elf", f"nude-body_{n}.stl")
+    _write_once(os.path.join(directory, rel), lambda p: write_stl(p, *elf_mesh(n)))
+    path = os.path.join(directory, name)
+    with open(path, "w") as fh:
+        fh.write(elf_sp(rel, max_depth))
+    return path

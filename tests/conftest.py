@@ -20,4 +20,7 @@ def scene_dir(tmp_path_factory):
     scenes.write_spheres_scene(d)
     # image-lit material_spheres.sp with a small synthetic HDR map (the 4k map is the bench's)
     scenes.write_material_spheres_scene(d, 96, 48, image="night_96x48.pfm")
+    # lucy.sp / elf.sp (PLY rotated by the scene, binary STL with vertex welding) at small sizes
+    scenes.write_lucy_scene(d, n=40, name="lucy_small.sp")
+    scenes.write_elf_scene(d, n=24, max_depth=16, name="elf_small.sp")
     return d

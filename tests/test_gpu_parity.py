@@ -166,7 +166,9 @@ def test_wavefront_rejects_other_integrators(scene_dir):
                                                       ("material_spheres.sp", 24, 48, "whitted", 3),
                                                       ("material_spheres.sp", 24, 48, "brute_force_iterative_rr", 3),
                                                       ("material_spheres_ibl.sp", 24, 48, "direct_lighting", 4),
-                                                      ("material_spheres_ibl.sp", 24, 48, "iterative_rrnee", 3)])
+                                                      ("material_spheres_ibl.sp", 24, 48, "iterative_rrnee", 3),
+                                                      ("lucy_small.sp", 40, 56, "direct_lighting", 3),
+                                                      ("elf_small.sp", 40, 56, "iterative_rrnee", 2)])
 def test_vs_reference_build_bitexact(scene_dir, scene, w, h, integrator, spp):
     # the HIP path against the reference's own code (oracle/_ref, built from its sources)
     from tests import test_oracle_vs_ref as R

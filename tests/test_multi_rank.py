@@ -25,7 +25,8 @@ def _worker(rank, world, port, scene_path, w, h, spp, result_path):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     import simplepath_amd as sp
     from simplepath_amd import shard
     from tests import _oracle
@@ -46,6 +47,7 @@ def _worker(rank, world, port, scene_path, w, h, spp, result_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [2, 3])
 def test_gather_frame_matches_single_process(scene_dir, tmp_path, world):
     import simplepath_amd as sp

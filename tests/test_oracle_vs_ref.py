@@ -109,3 +109,18 @@ def test_image_environment_light(ref, scene_dir, integrator):
     o = oracle_render(path, 24, 48, t, 4, ids)
     assert same(r, o), (integrator, float(np.abs(r - o).max()), int(np.sum(r != o)))
     assert r.max() > 0.0
+
+
+@pytest.mark.parametrize("scene,integrator,spp", [("lucy_small.sp", "direct_lighting", 3),
+                                                  ("elf_small.sp", "direct_lighting", 3),
+                                                  ("elf_small.sp", "iterative_rrnee", 2)])
+def test_figure_scenes(ref, scene_dir, scene, integrator, spp):
+    """lucy.sp (PLY with a scene rotation) and elf.sp (binary STL: std::map vertex welding,
+    file face normals; max_depth 16) with their constant environment lights."""
+    path = os.path.join(scene_dir, scene)
+    t = sp.string_to_integrator_type(integrator)
+    ids = np.arange(sp.TileScheduler(40, 56).get_num_tiles(), dtype=np.int32)
+    r = ref_render(ref, path, 40, 56, t, spp, ids)
+    o = oracle_render(path, 40, 56, t, spp, ids)
+    assert same(r, o), (scene, integrator, float(np.abs(r - o).max()))
+    assert r.max() > 0.0
