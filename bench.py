@@ -221,7 +221,7 @@ def roofline_of(stats, pixels, args, kernel_ms):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    if st.pipeline == 1:  # megakernel: one launch per frame
+    if st.pipeline == 1 or args.integrator != "direct_lighting":  # megakernel, or the sp_wpath rounds
         alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES
         achieved = alg / (kernel_ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

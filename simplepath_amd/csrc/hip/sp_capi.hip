@@ -228,6 +228,12 @@ struct sp_scene {
     hipEvent_t           ev_shade[2] = { nullptr, nullptr };
     int                  n_cu         = 0;
     hipEvent_t           ev0 = nullptr, ev1 = nullptr;
+    // multi-bounce wavefront (sp_wpath.hip)
+    void*                wp_buf     = nullptr;
+    size_t               wp_cap     = 0;
+    int32_t*             wp_ctl     = nullptr; // device int32[2]
+    int32_t*             wp_host    = nullptr; // pinned int32[2]
+    hipEvent_t           wp_ev[2]   = { nullptr, nullptr };
 
     void release()
     {
@@ -254,6 +260,12 @@ struct sp_scene {
         ev_fork = ev_join = nullptr;
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        if (wp_buf) (void)hipFree(wp_buf);
+        if (wp_ctl) (void)hipFree(wp_ctl);
+        if (wp_host) (void)hipHostFree(wp_host);
+        for (auto& e : wp_ev)
+            if (e) (void)hipEventDestroy(e);
+        wp_buf = nullptr; wp_cap = 0; wp_ctl = nullptr; wp_host = nullptr; wp_ev[0] = wp_ev[1] = nullptr;
         mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
         ev0 = ev1 = nullptr;
         mt_waves = 0; d_tiles_cap = 0;
@@ -709,13 +721,57 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     float      stage[4] = { 0, 0, 0, 0 };
     int pipeline = p->flags & 3;
     if (pipeline == 3) return fail(SP_ERR_ARG, "unknown pipeline flag");
-    const bool wave_ok = integ == SP_INTEGRATOR_DIRECT_LIGHTING && s->dev.n_lights <= spd::WF_MAX_LIGHTS;
-    if (pipeline == SP_PIPELINE_WAVEFRONT && !wave_ok)
-        return fail(SP_ERR_UNSUPPORTED, "wavefront pipeline supports DirectLighting with <= 32 lights");
+    const bool wave_ok  = integ == SP_INTEGRATOR_DIRECT_LIGHTING && s->dev.n_lights <= spd::WF_MAX_LIGHTS;
+    const bool wpath_ok = spd::wpath_supports(integ);
+    if (pipeline == SP_PIPELINE_WAVEFRONT && !wave_ok && !wpath_ok)
+        return fail(SP_ERR_UNSUPPORTED, "wavefront pipeline supports DirectLighting (<= 32 lights), "
+                                        "BruteForceIterative(RR) and IterativeRRNEE");
+    // AUTO: the split pipeline where it wins -- DirectLighting; the iterative integrators run the
+    // regenerating megakernel (sp_mega.hpp), which measured faster than sp_wpath
     if (pipeline == SP_PIPELINE_AUTO) pipeline = wave_ok ? SP_PIPELINE_WAVEFRONT : SP_PIPELINE_MEGAKERNEL;
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
     int launches = 0, parts_used = 1;
-    if (pipeline == SP_PIPELINE_WAVEFRONT) {
+    if (pipeline == SP_PIPELINE_WAVEFRONT && wpath_ok) {
+        const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
+        if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+        // tile slots in flight: enough waves to fill the chip several times over; each slot
+        // holds 64 pixel states (~27 KB with its mt19937_64 state), refilled from the tile list
+        int64_t slots = 32768;
+        if (const char* v = std::getenv("SP_PATH_SLOTS")) slots = std::max<int64_t>(1, std::atoll(v));
+        slots = std::min<int64_t>(slots, n_tiles);
+        const size_t need = spd::wpath_bytes_per_slot() * (size_t)slots + 16 * 256;
+        if (need > s->wp_cap) {
+            if (s->wp_buf) (void)hipFree(s->wp_buf);
+            s->wp_buf = nullptr;
+            s->wp_cap = 0;
+            SP_HIP(hipMalloc(&s->wp_buf, need));
+            s->wp_cap = need;
+        }
+        if (!s->wp_ctl) {
+            SP_HIP(hipMalloc(&s->wp_ctl, 2 * sizeof(int32_t)));
+            SP_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->wp_host), 2 * sizeof(int32_t), hipHostMallocDefault));
+            SP_HIP(hipEventCreateWithFlags(&s->wp_ev[0], hipEventDisableTiming));
+            SP_HIP(hipEventCreateWithFlags(&s->wp_ev[1], hipEventDisableTiming));
+        }
+        spd::WPathRun r{};
+        r.slots       = (int32_t)slots;
+        r.tile_ids    = p->tile_ids ? s->d_tiles : nullptr;
+        r.num_tiles   = n_tiles;
+        r.tiles_x     = (s->dev.width + 7) / 8;
+        r.spp         = p->samples_per_pixel;
+        r.integrator  = integ;
+        r.out         = d_out;
+        r.buf         = s->wp_buf;
+        r.ctl         = s->wp_ctl;
+        r.host_active = s->wp_host;
+        r.poll_ev[0]  = s->wp_ev[0];
+        r.poll_ev[1]  = s->wp_ev[1];
+        r.counters    = s->counters;
+        int iters = 0;
+        SP_HIP(hipEventRecord(s->ev0, stream));
+        SP_HIP(spd::wpath_render(s->dev, r, stream, &iters));
+        launches = 1 + 2 * iters + 1;
+    } else if (pipeline == SP_PIPELINE_WAVEFRONT) {
         const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
         if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         // Pixels in flight per pass: all requested tiles unless the state would exceed the budget

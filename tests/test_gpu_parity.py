@@ -157,8 +157,36 @@ def test_mandelbrot_full_frame_vs_reference(scene_dir):
 
 def test_wavefront_rejects_other_integrators(scene_dir):
     s = load(scene_dir, "bunny.sp", 16, 16, bvh=0)
-    with pytest.raises(sp.SimplePathError):
-        sp.render_tiles(s, "iterative_rrnee", 1, pipeline="wavefront")
+    for integ in ("whitted", "brute_force", "mandelbrot"):
+        with pytest.raises(sp.SimplePathError):
+            sp.render_tiles(s, integ, 1, pipeline="wavefront")
+
+
+@pytest.mark.parametrize("scene,bvh,w,h", [("bunny.sp", 0, 72, 40), ("material_spheres_ibl.sp", 1, 24, 48),
+                                           ("elf_small.sp", 0, 40, 56)])
+@pytest.mark.parametrize("integrator", ["brute_force_iterative", "brute_force_iterative_rr", "iterative_rrnee"])
+def test_path_wavefront_equals_megakernel(scene_dir, scene, bvh, w, h, integrator):
+    # trace/shade rounds over refilled tile slots (sp_wpath.hip) vs one lane per pixel
+    s = load(scene_dir, scene, w, h, bvh=bvh)
+    m, mst = sp.render_tiles(s, integrator, 5, pipeline="megakernel")
+    v, vst = sp.render_tiles(s, integrator, 5, pipeline="wavefront")
+    assert vst.pipeline == sp.PIPELINES["wavefront"]
+    assert np.array_equal(m.view(np.uint32), v.view(np.uint32)), rel_l2(v, m)
+    assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
+        (vst.rays, vst.shadow_rays, vst.samples, vst.rng_draws)
+
+
+def test_path_wavefront_slot_refill(scene_dir, monkeypatch):
+    # 3 slots for 45 tiles in a shuffled order: every slot is refilled many times
+    s = load(scene_dir, "bunny.sp", 72, 40, bvh=0)
+    ids = np.random.default_rng(5).permutation(sp.TileScheduler(72, 40).get_num_tiles()).astype(np.int32)
+    full, _ = sp.render_tiles(s, "iterative_rrnee", 3, ids, pipeline="wavefront")
+    monkeypatch.setenv("SP_PATH_SLOTS", "3")
+    few, fst = sp.render_tiles(s, "iterative_rrnee", 3, ids, pipeline="wavefront")
+    assert np.array_equal(few.view(np.uint32), full.view(np.uint32))
+    c, cst = _oracle.render(s, 5, 3, ids, variant="spm")
+    assert fst.rays == cst["rays"] and fst.samples == cst["samples"]
+    assert rel_l2(few, c) < REL_L2_TOL
 
 
 @pytest.mark.parametrize("scene,w,h,integrator,spp", [("bunny.sp", 64, 40, "direct_lighting", 4),
@@ -185,3 +213,15 @@ def test_vs_reference_build_bitexact(scene_dir, scene, w, h, integrator, spp):
     ids = np.arange(g.shape[0], dtype=np.int32)
     r = R.ref_render(L, os.path.join(scene_dir, scene), w, h, sp.string_to_integrator_type(integrator), spp, ids)
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), rel_l2(g, r)
+
+
+@pytest.mark.parametrize("integrator", ["brute_force_iterative", "brute_force_iterative_rr", "iterative_rrnee"])
+def test_megakernel_regen_equals_lockstep(scene_dir, monkeypatch, integrator):
+    # per-lane sample regeneration (SP_REGEN=1) vs the lock-step sample loop: same images and counts
+    s = load(scene_dir, "elf_small.sp", 40, 56, bvh=0)
+    monkeypatch.setenv("SP_REGEN", "1")
+    a, ast = sp.render_tiles(s, integrator, 4, pipeline="megakernel")
+    monkeypatch.setenv("SP_REGEN", "0")
+    b, bst = sp.render_tiles(s, integrator, 4, pipeline="megakernel")
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
+    assert (ast.rays, ast.shadow_rays, ast.samples, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.samples, bst.rng_draws)
