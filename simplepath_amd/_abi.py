@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libsimplepath_hip.so")
+# SP_LIB_PATH: an alternative build of the same library (experiments, e.g. compile-time variants)
+LIB_PATH = os.environ.get("SP_LIB_PATH") or os.path.join(_HERE, "_build", "libsimplepath_hip.so")
 
 SP_OK = 0
 SP_ERR_PARSE, SP_ERR_IO, SP_ERR_ARG, SP_ERR_HIP, SP_ERR_UNSUPPORTED, SP_ERR_STATE = -1, -2, -3, -4, -5, -6

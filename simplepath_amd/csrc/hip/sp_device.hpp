@@ -86,6 +86,8 @@ struct Scene {
     const float4*   pairs;     // pair-node copy of an SAH BVH (sp_path.hpp), nullptr otherwise
     const uint4*    qnodes;    // 16-byte quantised copy of an SAH BVH (sp_path.hpp), nullptr otherwise
     float           qorigin[3], qscale[3];
+    const uint4*    wnodes;    // 8-wide BVH (sp_host.hpp WideBvh), 5 per node; nullptr = binary walk
+    const float4*   wslot_tri; // 3 per wide-BVH primitive slot
     const float4*   slot_tri;  // 3 per slot
     const uint32_t* slot_code;
     const float*    normals;   // 3 per vertex
@@ -112,6 +114,7 @@ struct Scene {
     int             stack_words;   // LDS words per lane (2 per entry for the pair-node walk)
     int             packet;        // 1: BVHs shallow enough for the wave-coherent walk (sp_packet.hpp)
     int             ordered;       // 1: SAH BVH -- visit the near child (split axis, ray sign) first
+    int             wide_closest;  // 1: closest-hit queries walk the 8-wide BVH too (any-hit always does)
 };
 
 struct RenderArgs {

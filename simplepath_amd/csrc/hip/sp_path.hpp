@@ -266,13 +266,15 @@ __device__ __forceinline__ Isect finish_hit(const Scene& sc, const Hit& h, const
 }
 
 // Test one primitive code against the ray (closest-hit semantics: t <= tmax accepted).
-__device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h)
+__device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h,
+                                             const float4* tris = nullptr)
 {
-    const float4   q0   = sc.slot_tri[3 * slot]; // p0 | code
+    const float4*  st   = tris ? tris : sc.slot_tri;
+    const float4   q0   = st[3 * slot]; // p0 | code
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     if (kind == KIND_TRI) {
-        const float4 q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
+        const float4 q1 = st[3 * slot + 1], q2 = st[3 * slot + 2];
         float t, be, ga;
         if (tri_hit(q0, q1, q2, ray, tmin, h.t, t, be, ga)) {
             h.t = t; h.code = code; h.beta = be; h.gamma = ga;
@@ -287,13 +289,15 @@ __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, con
     return hit;
 }
 
-__device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, float tmax)
+__device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, float tmax,
+                                         const float4* tris = nullptr)
 {
-    const float4   q0   = sc.slot_tri[3 * slot]; // p0 | code
+    const float4*  st   = tris ? tris : sc.slot_tri;
+    const float4   q0   = st[3 * slot]; // p0 | code
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     if (kind == KIND_TRI) {
-        const float4 q1 = sc.slot_tri[3 * slot + 1], q2 = sc.slot_tri[3 * slot + 2];
+        const float4 q1 = st[3 * slot + 1], q2 = st[3 * slot + 2];
         float t, be, ga;
         return tri_hit(q0, q1, q2, ray, tmin, tmax, t, be, ga);
     }
@@ -450,6 +454,131 @@ __device__ __forceinline__ bool pair_any(const Scene& sc, const Ray& ray, float 
 }
 
 
+// ------------------------------------------------------------------------------ 8-wide BVH
+// One 80-byte fetch (5 x dwordx4) tests the boxes of up to 8 children, so a ray's chain of
+// dependent node fetches is about a third of the binary walk's.  Child boxes decode to
+// supersets of the exact boxes (outward rounding, sp_bvh.cpp build_wide): a box the exact test
+// accepts is accepted here too, so no primitive is missed; only the visiting order differs from
+// the binary SAH walk (closest hit: equal-distance ties; any hit: no change).  Stack entries are
+// child groups {first child << 8 | mask of pending children}: one entry per level.
+__device__ __forceinline__ bool wbox(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r, const f3& inv,
+                                     float tmin, float tmax, float& t0_out)
+{
+    return pair_box(lx, ly, lz, hx, hy, hz, r, inv, tmin, tmax, t0_out);
+}
+__device__ __forceinline__ float ubyte(uint32_t w, int k) { return (float)((w >> (8 * (k & 3))) & 0xffu); }
+
+struct WideHits {
+    uint32_t inner, leaf; // slot masks
+    int      nearest;     // inner slot with the smallest entry distance
+    uint32_t child_base, leaf_base, meta_lo, meta_hi;
+};
+__device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, const Ray& ray, const f3& inv, float tmin,
+                                               float tmax)
+{
+    const uint4*   np = sc.wnodes + 5 * (size_t)node;
+    const uint4    w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+    const float    px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
+    const float    sx = __uint_as_float((w0.w & 0xffu) << 23);
+    const float    sy = __uint_as_float(((w0.w >> 8) & 0xffu) << 23);
+    const float    sz = __uint_as_float(((w0.w >> 16) & 0xffu) << 23);
+    const uint32_t imask = w0.w >> 24;
+    WideHits       r;
+    r.inner = 0; r.leaf = 0; r.nearest = -1;
+    r.child_base = w1.x; r.leaf_base = w1.y; r.meta_lo = w1.z; r.meta_hi = w1.w;
+    float best = k_infinite;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t meta  = ((k < 4 ? w1.z : w1.w) >> (8 * (k & 3))) & 0xffu;
+        const bool     inner = (imask >> k) & 1u;
+        if (!inner && meta == 0u) continue;
+        const int   h  = k >> 2;
+        const float lx = fma_f(ubyte(h ? w2.y : w2.x, k), sx, px);
+        const float ly = fma_f(ubyte(h ? w2.w : w2.z, k), sy, py);
+        const float lz = fma_f(ubyte(h ? w3.y : w3.x, k), sz, pz);
+        const float hx = fma_f(ubyte(h ? w3.w : w3.z, k), sx, px);
+        const float hy = fma_f(ubyte(h ? w4.y : w4.x, k), sy, py);
+        const float hz = fma_f(ubyte(h ? w4.w : w4.z, k), sz, pz);
+        float       t0;
+        if (!wbox(lx, ly, lz, hx, hy, hz, ray, inv, tmin, tmax, t0)) continue;
+        if (inner) {
+            r.inner |= 1u << k;
+            if (t0 < best) { best = t0; r.nearest = k; }
+        } else {
+            r.leaf |= 1u << k;
+        }
+    }
+    return r;
+}
+
+__device__ __forceinline__ void wide_closest(const Scene& sc, const Ray& ray, float tmin, Hit& h, Stack st)
+{
+    const f3 inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp   = 0;
+    uint32_t node = 0;
+    while (true) {
+        const WideHits wh = wide_visit(sc, node, ray, inv, tmin, h.t);
+        for (uint32_t m = wh.leaf; m; m &= m - 1) {
+            const int      k    = __ffs(m) - 1;
+            const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
+            const uint32_t base = wh.leaf_base + (meta & 31u);
+            for (uint32_t j = 0; j < (meta >> 5); ++j) prim_closest(sc, base + j, ray, tmin, h, sc.wslot_tri);
+        }
+        if (wh.inner) {
+            const uint32_t rest = wh.inner & ~(1u << wh.nearest);
+            if (rest) {
+                st.s[sp * 64 + st.lane] = (wh.child_base << 8) | rest;
+                ++sp;
+            }
+            node = wh.child_base + (uint32_t)wh.nearest;
+            continue;
+        }
+        if (sp == 0) break;
+        const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
+        uint32_t       m = e & 0xffu;
+        const int      k = __ffs(m) - 1;
+        m &= m - 1;
+        if (m) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | m;
+        else --sp;
+        node = (e >> 8) + (uint32_t)k;
+    }
+}
+
+__device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    const f3 inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp   = 0;
+    uint32_t node = 0;
+    while (true) {
+        const WideHits wh = wide_visit(sc, node, ray, inv, tmin, tmax);
+        for (uint32_t m = wh.leaf; m; m &= m - 1) {
+            const int      k    = __ffs(m) - 1;
+            const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
+            const uint32_t base = wh.leaf_base + (meta & 31u);
+            for (uint32_t j = 0; j < (meta >> 5); ++j)
+                if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) return true;
+        }
+        if (wh.inner) {
+            const uint32_t rest = wh.inner & ~(1u << wh.nearest);
+            if (rest) {
+                st.s[sp * 64 + st.lane] = (wh.child_base << 8) | rest;
+                ++sp;
+            }
+            node = wh.child_base + (uint32_t)wh.nearest;
+            continue;
+        }
+        if (sp == 0) break;
+        const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
+        uint32_t       m = e & 0xffu;
+        const int      k = __ffs(m) - 1;
+        m &= m - 1;
+        if (m) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | m;
+        else --sp;
+        node = (e >> 8) + (uint32_t)k;
+    }
+    return false;
+}
+
 // ------------------------------------------------------------------------------ quantised BVH
 // 16-byte nodes: one dwordx4 fetch per visited node instead of two.  Boxes decode to a
 // superset of the exact boxes (outward rounding at build time), so the walk may visit a few
@@ -598,6 +727,7 @@ __device__ __forceinline__ Light uload_light(const Light* p)
 }
 
 // Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
+template <bool ALLOW_WIDE = true>
 __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     Hit h;
@@ -611,6 +741,10 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
         if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
     if (sc.n_nodes == 0) return h;
+    if (ALLOW_WIDE && sc.wide_closest) {
+        wide_closest(sc, ray, tmin, h, st);
+        return h;
+    }
     if (sc.qnodes) {
         qnode_closest(sc, ray, tmin, h, st);
         return h;
@@ -656,6 +790,7 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
         if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
     }
     if (sc.n_nodes == 0) return false;
+    if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
     if (sc.qnodes) return qnode_any(sc, ray, tmin, tmax, st);
     if (sc.pairs) return pair_any(sc, ray, tmin, tmax, st);
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);

@@ -34,6 +34,12 @@
 namespace spd {
 
 constexpr int WF_BLOCK = 256;
+#ifndef WF_PRIM_WAVES
+#define WF_PRIM_WAVES 1 // camera-ray kernel: no occupancy request (the binary walk needs few registers)
+#endif
+#ifndef WF_TRAV_WAVES
+#define WF_TRAV_WAVES 6 // waves per SIMD requested for the traversal kernels (profiles/r01 sweep)
+#endif
 constexpr int QSEG     = 32; // shadow-queue segments (one counter each, QSTRIDE words apart)
 constexpr int QSTRIDE  = 32;
 constexpr int QFETCH   = 16; // fetch counter of a segment: QFETCH words after its fill counter
@@ -148,7 +154,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_init(Scene sc, WaveArgs w)
 }
 
 // Primary query: Integrator::integrate's intersect_lights + intersect (Integrator.cpp:277-283).
-__global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uint32_t sample)
+// WIDE: closest hit on the 8-wide BVH (SP_WIDE_CLOSEST=1); the binary instantiation carries no
+// wide-walk code, so its register count (and occupancy) stays that of the binary walk.
+template <bool WIDE>
+__global__ void __launch_bounds__(WF_BLOCK, WF_PRIM_WAVES) wf_primary(Scene sc, WaveArgs w, uint32_t sample)
 {
     extern __shared__ uint32_t lds[];
     const int64_t p    = w.pb + (int64_t)blockIdx.x * WF_BLOCK + threadIdx.x;
@@ -178,7 +187,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_primary(Scene sc, WaveArgs w, uin
             const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
             lh = scene_intersect_lights(sc, ray, k_ray_epsilon, tmax, st);
             if (lh.hit) tmax = lh.t;
-            h = scene_intersect(sc, ray, k_ray_epsilon, tmax, st);
+            h = scene_intersect<WIDE>(sc, ray, k_ray_epsilon, tmax, st);
         }
         if (on) {
             rays = 1;
@@ -270,7 +279,7 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
 
 // Shadow queries, one queued ray per lane (static assignment; SP_SHADOW_DYN=0): direct_nee's
 // occlusion test (Integrator.cpp:297) -> vis[light][pixel].
-__global__ void __launch_bounds__(WF_BLOCK) wf_shadow(Scene sc, WaveArgs w)
+__global__ void __launch_bounds__(WF_BLOCK, WF_TRAV_WAVES) wf_shadow(Scene sc, WaveArgs w)
 {
     extern __shared__ uint32_t lds[];
     const int      lane  = threadIdx.x & 63;
@@ -606,7 +615,8 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         for (int k = 0; k < parts; ++k) {
             const WaveArgs& wi = (pw[k].diag && i == diag_sample) ? pw[k] : pd[k];
             hipStream_t     st = ps[k];
-            hipLaunchKernelGGL(wf_primary, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
+            if (sc.wide_closest) hipLaunchKernelGGL(wf_primary<true>, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
+            else hipLaunchKernelGGL(wf_primary<false>, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
             if (k == 0) mark();
             if (parts > 1 && (k == 1 || i > 0)) (void)hipStreamWaitEvent(st, shade_done[1 - k], 0);
             hipLaunchKernelGGL(shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, pd[k], i);

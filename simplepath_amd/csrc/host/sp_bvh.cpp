@@ -8,6 +8,7 @@
 #include "sp_host.hpp"
 
 #include <stdexcept>
+#include <cstring>
 
 #include <algorithm>
 #include <cmath>
@@ -233,6 +234,133 @@ Bvh build_bvh_sah(const std::vector<PrimBounds>& bounds, int max_leaf)
     out.nodes      = std::move(b.nodes);
     out.prim_order = std::move(b.ids);
     out.max_depth  = b.max_depth;
+    return out;
+}
+
+// ---------------------------------------------------------------- 8-wide collapse
+namespace {
+
+float node_area(const BvhNode& n)
+{
+    const float dx = n.hi[0] - n.lo[0], dy = n.hi[1] - n.lo[1], dz = n.hi[2] - n.lo[2];
+    if (!(dx >= 0.0f)) return 0.0f;
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+
+struct WideBuilder {
+    const Bvh& b;
+    WideBvh&   out;
+
+    bool is_leaf(uint32_t i) const { return (b.nodes[i].b & BVH_LEAF) != 0; }
+    uint32_t left(uint32_t i) const { return b.nodes[i].a & BVH_CHILD_MASK; }
+    uint32_t right(uint32_t i) const { return b.nodes[i].b; }
+
+    // Quantise one axis of the children onto origin p with the smallest power-of-two step that
+    // keeps every decoded box (fma(q, step, p), as the device decodes it) outside the exact one.
+    void quantise(const float* lo, const float* hi, int n, float p, float extent, uint8_t* qlo, uint8_t* qhi,
+                  uint8_t& ebyte)
+    {
+        int k = -126;
+        if (extent > 0.0f) {
+            int e2;
+            std::frexp(extent / 254.0f, &e2); // extent/254 < 2^e2
+            k = std::max(e2, -126);
+        }
+        for (;; ++k) {
+            const float step = std::ldexp(1.0f, k);
+            bool        ok   = true;
+            for (int c = 0; c < n && ok; ++c) {
+                float ql = std::floor((lo[c] - p) / step);
+                ql       = std::min(std::max(ql, 0.0f), 255.0f);
+                while (ql > 0.0f && std::fma(ql, step, p) > lo[c]) ql -= 1.0f;
+                float qh = std::ceil((hi[c] - p) / step);
+                qh       = std::min(std::max(qh, 0.0f), 255.0f);
+                while (qh < 255.0f && std::fma(qh, step, p) < hi[c]) qh += 1.0f;
+                if (std::fma(ql, step, p) > lo[c] || std::fma(qh, step, p) < hi[c]) ok = false;
+                qlo[c] = (uint8_t)ql;
+                qhi[c] = (uint8_t)qh;
+            }
+            if (ok) {
+                ebyte = (uint8_t)(k + 127);
+                return;
+            }
+            if (k >= 127) throw std::runtime_error("wide BVH: cannot quantise child boxes");
+        }
+    }
+
+    void emit(uint32_t wi, uint32_t bi, int depth)
+    {
+        out.depth = std::max(out.depth, depth);
+        // collapse: open the internal child of largest area until 8 children
+        std::vector<uint32_t> kids;
+        if (is_leaf(bi)) kids.push_back(bi);
+        else { kids.push_back(left(bi)); kids.push_back(right(bi)); }
+        while (kids.size() < 8) {
+            int   best = -1;
+            float ba   = -1.0f;
+            for (size_t i = 0; i < kids.size(); ++i)
+                if (!is_leaf(kids[i]) && node_area(b.nodes[kids[i]]) > ba) { ba = node_area(b.nodes[kids[i]]); best = (int)i; }
+            if (best < 0) break;
+            const uint32_t n = kids[(size_t)best];
+            kids[(size_t)best] = left(n);
+            kids.insert(kids.begin() + best + 1, right(n));
+        }
+        std::vector<uint32_t> inner, leaves;
+        for (uint32_t k : kids) (is_leaf(k) ? leaves : inner).push_back(k);
+        std::vector<uint32_t> order(inner);
+        order.insert(order.end(), leaves.begin(), leaves.end());
+        const int n = (int)order.size();
+        float     lo[3][8], hi[3][8], ulo[3], uhi[3];
+        for (int a = 0; a < 3; ++a) { ulo[a] = INFINITY; uhi[a] = -INFINITY; }
+        for (int c = 0; c < n; ++c)
+            for (int a = 0; a < 3; ++a) {
+                lo[a][c] = b.nodes[order[(size_t)c]].lo[a];
+                hi[a][c] = b.nodes[order[(size_t)c]].hi[a];
+                ulo[a]   = std::min(ulo[a], lo[a][c]);
+                uhi[a]   = std::max(uhi[a], hi[a][c]);
+            }
+        uint8_t q[6][8] = {};
+        uint8_t eb[3];
+        for (int a = 0; a < 3; ++a) quantise(lo[a], hi[a], n, ulo[a], uhi[a] - ulo[a], q[a], q[3 + a], eb[a]);
+        const uint32_t child_base = (uint32_t)(out.words.size() / 20);
+        out.words.resize(out.words.size() + 20 * inner.size());
+        const uint32_t leaf_base = (uint32_t)out.slot_of.size();
+        uint8_t        meta[8]   = {};
+        for (int c = (int)inner.size(); c < n; ++c) {
+            const BvhNode& lf  = b.nodes[order[(size_t)c]];
+            const uint32_t cnt = lf.b & ~BVH_LEAF;
+            const uint32_t off = (uint32_t)out.slot_of.size() - leaf_base;
+            if (cnt == 0 || cnt > 7 || off > 31) throw std::runtime_error("wide BVH: leaf does not fit a meta byte");
+            meta[c] = (uint8_t)(cnt << 5 | off);
+            for (uint32_t j = 0; j < cnt; ++j) out.slot_of.push_back((int32_t)(lf.a + j));
+        }
+        uint32_t* w = &out.words[(size_t)wi * 20];
+        std::memcpy(&w[0], &ulo[0], 4);
+        std::memcpy(&w[1], &ulo[1], 4);
+        std::memcpy(&w[2], &ulo[2], 4);
+        const uint32_t imask = (1u << inner.size()) - 1u;
+        w[3] = (uint32_t)eb[0] | (uint32_t)eb[1] << 8 | (uint32_t)eb[2] << 16 | imask << 24;
+        w[4] = child_base;
+        w[5] = leaf_base;
+        w[6] = (uint32_t)meta[0] | (uint32_t)meta[1] << 8 | (uint32_t)meta[2] << 16 | (uint32_t)meta[3] << 24;
+        w[7] = (uint32_t)meta[4] | (uint32_t)meta[5] << 8 | (uint32_t)meta[6] << 16 | (uint32_t)meta[7] << 24;
+        for (int r = 0; r < 6; ++r)
+            for (int h = 0; h < 2; ++h)
+                w[8 + 2 * r + h] = (uint32_t)q[r][4 * h] | (uint32_t)q[r][4 * h + 1] << 8 | (uint32_t)q[r][4 * h + 2] << 16 |
+                                   (uint32_t)q[r][4 * h + 3] << 24;
+        for (size_t i = 0; i < inner.size(); ++i) emit(child_base + (uint32_t)i, inner[i], depth + 1);
+    }
+};
+
+} // namespace
+
+WideBvh build_wide(const Bvh& bvh)
+{
+    WideBvh out;
+    if (bvh.nodes.empty()) return out;
+    out.words.resize(20);
+    WideBuilder wb{ bvh, out };
+    wb.emit(0, 0, 1);
     return out;
 }
 

@@ -154,6 +154,20 @@ Bvh build_bvh_reference(const std::vector<PrimBounds>& bounds);
 // Binned SAH construction (product default).
 Bvh build_bvh_sah(const std::vector<PrimBounds>& bounds, int max_leaf = 4);
 
+// 8-wide BVH collapsed from a binary SAH BVH (sp_bvh.cpp build_wide): 80-byte nodes with
+// child boxes quantised outward on a per-node power-of-two grid, internal children first.
+// Layout per node (5 x 16 bytes, u32 words):
+//   [0..2] grid origin xyz (float bits)  [3] exponent bytes ex | ey << 8 | ez << 16 | imask << 24
+//   [4] first child node  [5] first primitive slot  [6..7] meta bytes of slots 0-7
+//       (leaf: count << 5 | offset from [5]; 0 = empty slot; internal slots 0..ni-1 per imask)
+//   [8..19] quantised bytes: lo_x[8] lo_y[8] lo_z[8] hi_x[8] hi_y[8] hi_z[8] (4 per word)
+struct WideBvh {
+    std::vector<uint32_t> words;   // 20 per node
+    std::vector<int32_t>  slot_of; // wide primitive slot -> binary primitive slot
+    int                   depth = 0;
+};
+WideBvh build_wide(const Bvh& bvh);
+
 // libstdc++ std::partition on a bidirectional range, returning the split point.
 template <typename T, typename Pred>
 size_t stl_partition(std::vector<T>& v, size_t first, size_t last, Pred pred)

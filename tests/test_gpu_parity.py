@@ -225,3 +225,18 @@ def test_megakernel_regen_equals_lockstep(scene_dir, monkeypatch, integrator):
     b, bst = sp.render_tiles(s, integrator, 4, pipeline="megakernel")
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
     assert (ast.rays, ast.shadow_rays, ast.samples, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.samples, bst.rng_draws)
+
+
+@pytest.mark.parametrize("scene,w,h", [("bunny.sp", 64, 40), ("lucy_small.sp", 40, 56), ("elf_small.sp", 40, 56)])
+def test_wide_bvh_vs_binary(scene_dir, monkeypatch, scene, w, h):
+    # 8-wide quantised BVH (SAH default) vs the binary SAH walk: same rays traced (any-hit is
+    # exact, closest hit differs only on exactly equal distances) and the oracle tolerance
+    monkeypatch.setenv("SP_WIDE", "0")
+    s0 = load(scene_dir, scene, w, h, bvh=0)
+    b, bst = sp.render_tiles(s0, "direct_lighting", 4)
+    monkeypatch.setenv("SP_WIDE", "1")
+    s1 = load(scene_dir, scene, w, h, bvh=0)
+    a, ast = sp.render_tiles(s1, "direct_lighting", 4)
+    c, _ = _oracle.render(s1, 6, 4, variant="spm")
+    assert rel_l2(a, c) < REL_L2_TOL and rel_l2(b, c) < REL_L2_TOL
+    assert np.mean(np.all(a == b, axis=-1)) > 0.999
