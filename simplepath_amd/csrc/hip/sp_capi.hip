@@ -34,7 +34,7 @@ int fail(int code, const std::string& msg)
         if (e__ != hipSuccess) return fail(SP_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e__)); \
     } while (0)
 
-constexpr int MAX_RECURSION = 32; // sp_path.hpp integrate_bruteforce / integrate_whitted
+constexpr int MAX_RECURSION = 32; // sp_path.hpp integrate_bruteforce / integrate_whitted in-register levels
 
 uint32_t code_of(int kind, int index) { return ((uint32_t)kind << spd::CODE_SHIFT) | (uint32_t)index; }
 
@@ -228,6 +228,8 @@ struct sp_scene {
     hipEvent_t           ev_shade[2] = { nullptr, nullptr };
     int                  n_cu         = 0;
     hipEvent_t           ev0 = nullptr, ev1 = nullptr;
+    void*                deep_buf   = nullptr; // recursive integrators beyond MAX_RECURSION levels
+    size_t               deep_cap   = 0;
     // multi-bounce wavefront (sp_wpath.hip)
     void*                wp_buf     = nullptr;
     size_t               wp_cap     = 0;
@@ -261,6 +263,8 @@ struct sp_scene {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (wp_buf) (void)hipFree(wp_buf);
+        if (deep_buf) (void)hipFree(deep_buf);
+        deep_buf = nullptr; deep_cap = 0;
         if (wp_ctl) (void)hipFree(wp_ctl);
         if (wp_host) (void)hipHostFree(wp_host);
         for (auto& e : wp_ev)
@@ -717,8 +721,6 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = s->host->integrator;
     if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = SP_INTEGRATOR_DIRECT_LIGHTING; // main.cpp:390
     if (integ < SP_INTEGRATOR_MANDELBROT || integ > SP_INTEGRATOR_WHITTED) return fail(SP_ERR_ARG, "Unknown integrator type");
-    if ((integ == SP_INTEGRATOR_BRUTE_FORCE || integ == SP_INTEGRATOR_WHITTED) && s->host->max_depth > MAX_RECURSION)
-        return fail(SP_ERR_UNSUPPORTED, "recursive integrators support max_depth <= 32");
     int64_t total;
     sp_tile_count(s->dev.width, s->dev.height, &total);
     const int64_t n_tiles = p->tile_ids ? p->num_tiles : total;
@@ -943,6 +945,22 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
         a.tile_counter = s->tile_counter;
         a.mt_state     = s->mt_state;
         a.counters     = s->counters;
+        // BruteForce / Whitted recursion deeper than the in-register arrays: global level records
+        a.deep        = nullptr;
+        a.deep_stride = 0;
+        if ((integ == SP_INTEGRATOR_BRUTE_FORCE || integ == SP_INTEGRATOR_WHITTED) && s->dev.max_depth > MAX_RECURSION) {
+            const size_t lanes = waves * 64; // persistent waves of this launch (4 per block)
+            const size_t bytes = lanes * ((size_t)s->dev.max_depth + 1) * 5 * sizeof(float);
+            if (bytes > s->deep_cap) {
+                if (s->deep_buf) (void)hipFree(s->deep_buf);
+                s->deep_buf = nullptr;
+                s->deep_cap = 0;
+                SP_HIP(hipMalloc(&s->deep_buf, bytes));
+                s->deep_cap = bytes;
+            }
+            a.deep        = static_cast<float*>(s->deep_buf);
+            a.deep_stride = lanes;
+        }
         SP_HIP(hipEventRecord(s->ev0, stream));
         SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
         launches = 1;

@@ -127,6 +127,8 @@ struct RenderArgs {
     int32_t*        tile_counter;
     uint64_t*       mt_state;
     unsigned long long* counters; // [rays, shadow_rays, samples, draws]
+    float*          deep;       // recursive integrators, max_depth > 32: per-lane level records
+    size_t          deep_stride;// lanes of the launch (= blocks * 256)
 };
 
 } // namespace spd

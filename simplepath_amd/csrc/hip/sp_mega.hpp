@@ -60,6 +60,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
             rng_seed(rng, pix_seed ^ 0xb0ae9d99u);          // get_integrator_sampler (main.cpp:73)
             const uint32_t seed2d = pix_seed ^ 0x6184faf4u; // RSequenceSampler m_seed_2D (main.cpp:67)
             Ctx c{ sc, rng, q, st, 0u, 0u };
+            if (args.deep) {
+                c.deep    = args.deep + gwave * 64 + lane;
+                c.dstride = args.deep_stride;
+            }
             for (uint32_t i = 0; i < args.spp; ++i) {
                 rng_prepare(rng);
                 // RSequenceSampler::get_next_2D (math/Sampler.h:158) with count i

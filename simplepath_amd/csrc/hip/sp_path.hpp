@@ -1605,6 +1605,10 @@ struct Ctx {
     const Rsq&   q;
     Stack        st;
     uint32_t     rays, shadow;
+    // recursive integrators with max_depth > MAX_RECURSION: per-level records in global memory,
+    // record k of this lane at deep[k * dstride] (level-major, lanes contiguous)
+    float*       deep    = nullptr;
+    size_t       dstride = 0;
 };
 
 __device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float tmax)
@@ -1713,7 +1717,14 @@ __device__ __forceinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
     float pdfv[MAX_RECURSION];
     int   depth = 0;
     rgb   Lend  = mkc(0, 0, 0);
-    const int maxd = c.sc.max_depth < MAX_RECURSION ? c.sc.max_depth : MAX_RECURSION;
+    // levels beyond the register/scratch arrays go to the lane's global records (5 floats each)
+    const bool deep = c.deep != nullptr;
+    const int  maxd = deep ? c.sc.max_depth : (c.sc.max_depth < MAX_RECURSION ? c.sc.max_depth : MAX_RECURSION);
+    auto put = [&](int k, float cs, rgb col, float pdf) {
+        if (!deep) { cosv[k] = cs; colv[k] = col; pdfv[k] = pdf; return; }
+        float* d = c.deep + (size_t)k * 5 * c.dstride;
+        d[0] = cs; d[c.dstride] = col.r; d[2 * c.dstride] = col.g; d[3 * c.dstride] = col.b; d[4 * c.dstride] = pdf;
+    };
     while (true) {
         if (depth >= maxd) { Lend = mkc(0, 0, 0); break; }
         rng_prepare(c.rng);
@@ -1723,9 +1734,7 @@ __device__ __forceinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
             const f3      n  = qr.is.n;
             const MSample s  = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
             if (s.pdf == 0.0f || cblack(s.color)) { Lend = mkc(0, 0, 0); break; }
-            cosv[depth] = dot(s.dir, n);
-            colv[depth] = s.color;
-            pdfv[depth] = s.pdf;
+            put(depth, dot(s.dir, n), s.color, s.pdf);
             ray.o       = ray_at(ray, qr.is.t);
             ray.d       = s.dir;
             ++depth;
@@ -1737,7 +1746,16 @@ __device__ __forceinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
             break;
         }
     }
-    for (int k = depth - 1; k >= 0; --k) Lend = cdivs(cmul(cscale(Lend, cosv[k]), colv[k]), pdfv[k]);
+    for (int k = depth - 1; k >= 0; --k) {
+        float cs, pdf;
+        rgb   col;
+        if (!deep) { cs = cosv[k]; col = colv[k]; pdf = pdfv[k]; }
+        else {
+            const float* d = c.deep + (size_t)k * 5 * c.dstride;
+            cs = d[0]; col = mkc(d[c.dstride], d[2 * c.dstride], d[3 * c.dstride]); pdf = d[4 * c.dstride];
+        }
+        Lend = cdivs(cmul(cscale(Lend, cs), col), pdf);
+    }
     return Lend;
 }
 
@@ -1745,12 +1763,23 @@ __device__ __forceinline__ rgb integrate_bruteforce(Ctx& c, Ray ray)
 // L_k += do_integrate(child) folds right-nested: L_0 + (L_1 + (L_2 + ...)).
 __device__ __forceinline__ rgb integrate_whitted(Ctx& c, Ray ray)
 {
-    rgb       Lv[MAX_RECURSION + 1];
-    int       depth = 0;
-    const int maxd  = c.sc.max_depth < MAX_RECURSION ? c.sc.max_depth : MAX_RECURSION;
+    rgb        Lv[MAX_RECURSION + 1];
+    int        depth = 0;
+    const bool deep  = c.deep != nullptr; // levels in the lane's global records (3 floats each)
+    const int  maxd  = deep ? c.sc.max_depth : (c.sc.max_depth < MAX_RECURSION ? c.sc.max_depth : MAX_RECURSION);
+    auto put = [&](int k, rgb L) {
+        if (!deep) { Lv[k] = L; return; }
+        float* d = c.deep + (size_t)k * 3 * c.dstride;
+        d[0] = L.r; d[c.dstride] = L.g; d[2 * c.dstride] = L.b;
+    };
+    auto get = [&](int k) {
+        if (!deep) return Lv[k];
+        const float* d = c.deep + (size_t)k * 3 * c.dstride;
+        return mkc(d[0], d[c.dstride], d[2 * c.dstride]);
+    };
     while (true) {
         rgb L = mkc(0, 0, 0);
-        if (depth >= maxd) { Lv[depth] = L; break; }
+        if (depth >= maxd) { put(depth, L); break; }
         rng_prepare(c.rng);
         const Query qr   = trace(c, ray, k_ray_epsilon, k_infinite);
         bool        more = false;
@@ -1768,12 +1797,12 @@ __device__ __forceinline__ rgb integrate_whitted(Ctx& c, Ray ray)
         } else if (qr.lh.hit) {
             L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(c.sc, qr.lh, ray.d, c.q)));
         }
-        Lv[depth] = L;
+        put(depth, L);
         if (!more) break;
         ++depth;
     }
-    rgb acc = Lv[depth];
-    for (int k = depth - 1; k >= 0; --k) acc = cadd(Lv[k], acc);
+    rgb acc = get(depth);
+    for (int k = depth - 1; k >= 0; --k) acc = cadd(get(k), acc);
     return acc;
 }
 

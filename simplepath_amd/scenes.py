@@ -565,3 +565,69 @@ def write_elf_scene(directory: str, n: int = 290, max_depth: int | None = 16, na
     with open(path, "w") as fh:
         fh.write(elf_sp(rel, max_depth))
     return path
+
+
+def closed_room_sp(max_depth: int = 40) -> str:
+    """A camera inside a closed box of six inward-facing lambertian planes with a clearcoat
+    ball and a sphere light: no path escapes, so the recursive integrators reach max_depth."""
+    walls = [("0.0 -2.0 0.0", None), ("0.0 2.0 0.0", "1 0 0 180"), ("-2.0 0.0 0.0", "0 0 1 -90"),
+             ("2.0 0.0 0.0", "0 0 1 90"), ("0.0 0.0 -6.0", "1 0 0 90"), ("0.0 0.0 2.0", "1 0 0 -90")]
+    planes = ""
+    for t, r in walls:
+        planes += "plane {\n    material: \"wall\"\n    translate: %s\n" % t
+        if r:
+            planes += "    rotate: %s\n" % r
+        planes += "}\n\n"
+    return f"""version: 1
+
+scene_parameters {{
+    output_file_name: "room.pfm"
+    width: 16
+    height: 16
+    max_depth: {max_depth}
+}}
+
+perspective_camera {{
+    origin: 0.0 0.0 0.0
+    look_at: 0.0 0.0 -1.0
+    fov: 60
+}}
+
+material_lambertian {{
+    name: "wall"
+    diffuse: 0.9 0.85 0.8
+}}
+
+material_glossy {{
+    name: "ball_base"
+    diffuse: 0.8 0.3 0.3
+    ior: 1.5
+    roughness: 0.3
+}}
+
+material_clearcoat {{
+    name: "ball"
+    base: "ball_base"
+    ior: 1.5
+    color: 1.0 1.0 1.0
+}}
+
+{planes}sphere {{
+    translate: 0.0 -1.0 -4.0
+    material: "ball"
+}}
+
+sphere_light {{
+    translate: 0.0 1.5 -3.0
+    scale: 0.5 0.5 0.5
+    radiance: 5.0 5.0 5.0
+}}
+"""
+
+
+def write_closed_room_scene(directory: str, max_depth: int = 40, name: str = "closed_room.sp") -> str:
+    os.makedirs(directory, exist_ok=True)
+    path = os.path.join(directory, name)
+    with open(path, "w") as fh:
+        fh.write(closed_room_sp(max_depth))
+    return path

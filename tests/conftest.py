@@ -23,4 +23,6 @@ def scene_dir(tmp_path_factory):
     # lucy.sp / elf.sp (PLY rotated by the scene, binary STL with vertex welding) at small sizes
     scenes.write_lucy_scene(d, n=40, name="lucy_small.sp")
     scenes.write_elf_scene(d, n=24, max_depth=16, name="elf_small.sp")
+    # recursion deeper than the device's in-register levels (32)
+    scenes.write_closed_room_scene(d, max_depth=40)
     return d

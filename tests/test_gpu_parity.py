@@ -240,3 +240,15 @@ def test_wide_bvh_vs_binary(scene_dir, monkeypatch, scene, w, h):
     c, _ = _oracle.render(s1, 6, 4, variant="spm")
     assert rel_l2(a, c) < REL_L2_TOL and rel_l2(b, c) < REL_L2_TOL
     assert np.mean(np.all(a == b, axis=-1)) > 0.999
+
+
+@pytest.mark.parametrize("integrator", ["brute_force", "whitted"])
+def test_deep_recursion_bitexact(scene_dir, integrator):
+    # max_depth 40 > the 32 in-register recursion levels: deeper levels live in global records
+    s = load(scene_dir, "closed_room.sp", 16, 16, bvh=1)
+    g, gst = sp.render_tiles(s, integrator, 2)
+    c, cst = _oracle.render(s, sp.string_to_integrator_type(integrator), 2, variant="glibc")
+    assert gst.rays == cst["rays"]
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
+    if integrator == "brute_force":
+        assert gst.rays > 16 * 16 * 2 * 20  # mean path length > 20: many paths go past level 32

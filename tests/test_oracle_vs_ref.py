@@ -124,3 +124,15 @@ def test_figure_scenes(ref, scene_dir, scene, integrator, spp):
     o = oracle_render(path, 40, 56, t, spp, ids)
     assert same(r, o), (scene, integrator, float(np.abs(r - o).max()))
     assert r.max() > 0.0
+
+
+@pytest.mark.parametrize("integrator", ["brute_force", "whitted", "iterative_rrnee"])
+def test_deep_recursion(ref, scene_dir, integrator):
+    """Closed room, max_depth 40: recursive paths run to the depth limit."""
+    path = os.path.join(scene_dir, "closed_room.sp")
+    t = sp.string_to_integrator_type(integrator)
+    ids = np.arange(sp.TileScheduler(16, 16).get_num_tiles(), dtype=np.int32)
+    r = ref_render(ref, path, 16, 16, t, 2, ids)
+    o = oracle_render(path, 16, 16, t, 2, ids)
+    assert same(r, o), (integrator, float(np.abs(r - o).max()))
+    assert r.max() > 0.0
