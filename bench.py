@@ -161,7 +161,16 @@ def main():
     cpu = None
     parity = None
     if not args.no_cpu:
-        cpu, parity = cpu_baseline(scene, path, integ, args, out if world == 1 else None, my_tiles)
+        # the reference library logs to stdout (base/Logger.cpp); keep stdout for the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            cpu, parity = cpu_baseline(scene, path, integ, args, out if world == 1 else None, my_tiles)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     line = {
         "metric": "Mrays/sec (+ Msamples/sec) at fixed spp; per-pixel L2 vs CPU ref",
@@ -188,6 +197,7 @@ def main():
         "parity": parity,
     }
     print(json.dumps(line), flush=True)
+    os.dup2(2, 1)  # exit-time log summaries of the reference library go to stderr
     if dist is not None:
         dist.destroy_process_group()
 

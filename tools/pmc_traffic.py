@@ -16,13 +16,21 @@ import os
 import sys
 
 
+def kernel_key(name):
+    """'void spd::wf_shade<4>(spd::Scene, ...)' -> 'spd::wf_shade' (template instances merged)."""
+    k = name.split("(")[0]
+    if k.startswith("void "):
+        k = k[5:]
+    return k.split("<")[0]
+
+
 def per_kernel(root, counter):
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row["Counter_Name"] == counter:
-                    vals[row["Kernel_Name"].split("(")[0]].append(float(row["Counter_Value"]))
+                    vals[kernel_key(row["Kernel_Name"])].append(float(row["Counter_Value"]))
     return vals
 
 
