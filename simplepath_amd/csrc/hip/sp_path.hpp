@@ -1333,12 +1333,126 @@ __device__ __forceinline__ MSample mf_sample(const Material& m, f3 wo, Rng& rng,
     r.props = PROP_GLOSSY | PROP_REFLECTIVE;
     return r;
 }
-// BRDF::rho_impl default (materials/Material.h:299) for the microfacet lobe
+// BRDF::rho_impl default (materials/Material.h:299) for the microfacet lobe.  All 16 samples
+// share wo, so everything beckmann_sample / beckmann_sample11 / the Smith lambda compute from wo
+// alone is evaluated once (BeckPre) -- the same expressions on the same inputs, so every sample
+// is bit-identical to mf_sample's; only the per-sample work (U1, U2 onwards) stays in the loop.
+struct BeckPre {
+    bool  flip, steep;
+    f3    st;
+    float cphi, sphi;
+    float tan_theta_i, c0, fit, normalization, sqrt_pi_inv;
+    float lam_wo;
+};
+__device__ __forceinline__ BeckPre beck_pre(const Material& m, f3 wo, const Rsq& q)
+{
+    BeckPre p;
+    p.flip               = wo.y < 0.0f;
+    const f3 wi          = p.flip ? neg(wo) : wo;
+    p.st                 = normalize(mk(m.alpha_x * wi.x, wi.y, m.alpha_y * wi.z), q);
+    p.cphi               = cos_phi(p.st);
+    p.sphi               = sin_phi(p.st);
+    const float cos_t    = p.st.y;
+    p.steep              = cos_t > .9999f;
+    p.tan_theta_i = p.c0 = p.fit = p.normalization = p.sqrt_pi_inv = 0.0f;
+    if (!p.steep) {
+        const float sin_theta_i = sqrt_f(std_max(0.0f, 1.0f - cos_t * cos_t));
+        p.tan_theta_i           = sin_theta_i / cos_t;
+        const float cot_theta_i = 1.0f / p.tan_theta_i;
+        p.c0                    = lm_erff(cot_theta_i);
+        const float theta_i     = lm_acosf(cos_t);
+        p.fit                   = 1.0f + theta_i * (-0.876f + theta_i * (0.4265f - 0.0594f * theta_i));
+        p.sqrt_pi_inv           = 1.0f / sqrt_f(k_pi);
+        p.normalization = 1.0f / (1.0f + p.c0 + p.sqrt_pi_inv * p.tan_theta_i * lm_expf(-cot_theta_i * cot_theta_i));
+    }
+    p.lam_wo = beck_lambda(m, wo);
+    return p;
+}
+// beckmann_sample11 (materials/Material.cpp:14) from the precomputed wo terms
+__device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, float U2)
+{
+    P2 s;
+    if (p.steep) {
+        const float r  = sqrt_f(-lm_logf(1.0f - U1));
+        const float sp = lm_sinf(2.0f * k_pi * U2);
+        const float cp = lm_cosf(2.0f * k_pi * U2);
+        s.x = r * cp;
+        s.y = r * sp;
+        return s;
+    }
+    float       a        = -1.0f;
+    float       c        = p.c0;
+    const float sample_x = std_max(U1, 1e-6f);
+    float       b        = c - (1.0f + c) * lm_powf(1.0f - sample_x, p.fit);
+    for (int it = 0; it < 9; ++it) {
+        if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+        const float inv_erf = erfinv(b);
+        const float value =
+            p.normalization * (1.0f + b + p.sqrt_pi_inv * p.tan_theta_i * lm_expf(-inv_erf * inv_erf)) - sample_x;
+        const float derivative = p.normalization * (1.0f - inv_erf * p.tan_theta_i);
+        if (abs_f(value) < 1e-5f) break;
+        if (value > 0) c = b;
+        else a = b;
+        b -= value / derivative;
+    }
+    s.x = erfinv(b);
+    s.y = erfinv(2.0f * std_max(U2, 1e-6f) - 1.0f);
+    return s;
+}
+// mf_sample with the precomputed wo terms (draw order: U2, then U1)
+__device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPre& p, f3 wo, Rng& rng, const Rsq& q)
+{
+    MSample r;
+    r.color = mkc(0, 0, 0);
+    r.dir   = mk(0, 0, 0);
+    r.pdf   = 0.0f;
+    r.props = 0;
+    if (wo.y == 0.0f) return r;
+    const float U2 = next1D(rng);
+    const float U1 = next1D(rng);
+    P2          sl = beckmann_sample11_pre(p, U1, U2);
+    const float tmp = p.cphi * sl.x - p.sphi * sl.y;
+    sl.y            = p.sphi * sl.x + p.cphi * sl.y;
+    sl.x            = tmp;
+    sl.x            = m.alpha_x * sl.x;
+    sl.y            = m.alpha_y * sl.y;
+    f3 wh = normalize(mk(-sl.x, 1.0f, -sl.y), q);
+    if (p.flip) wh = neg(wh);
+    const float dp = dot(wo, wh);
+    if (dp < 0.0f) return r;
+    const f3 wi = add(neg(wo), scale(2.0f * dot(wo, wh), wh));
+    if (!same_hemisphere(wo, wi)) return r;
+    // beck_pdf(m, wo, wh) with G1(wo) = 1 / (1 + lambda(wo))
+    const float bpdf = m.sample_visible_area ? beck_D(m, wh) * (1.0f / (1.0f + p.lam_wo)) * abs_f(dot(wo, wh)) / abs_f(wo.y)
+                                             : beck_D(m, wh) * abs_f(wh.y);
+    r.pdf = bpdf / (4.0f * dp);
+    // mf_eval(m, wo, wi) with G = 1 / (1 + lambda(wo) + lambda(wi))
+    {
+        const float ao = abs_f(wo.y), ai = abs_f(wi.y);
+        if (ai == 0.0f || ao == 0.0f) {
+            r.color = mkc(0, 0, 0);
+        } else {
+            f3 h = add(wi, wo);
+            if (h.x == 0.0f && h.y == 0.0f && h.z == 0.0f) {
+                r.color = mkc(0, 0, 0);
+            } else {
+                h             = normalize(h, q);
+                const float f = fresnel_dielectric(dot(wi, h), 1.0f, m.microfacet_ior);
+                const float G = 1.0f / (1.0f + p.lam_wo + beck_lambda(m, wi));
+                r.color = cdivs(cscale(cscale(cscale(m.microfacet_r, beck_D(m, h)), G), f), 4.0f * ai * ao);
+            }
+        }
+    }
+    r.dir   = wi;
+    r.props = PROP_GLOSSY | PROP_REFLECTIVE;
+    return r;
+}
 __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
-    rgb r = mkc(0, 0, 0);
+    const BeckPre p = beck_pre(m, wo, q);
+    rgb           r = mkc(0, 0, 0);
     for (unsigned i = 0; i < 16u; ++i) {
-        const MSample s = mf_sample(m, wo, rng, q);
+        const MSample s = mf_sample_pre(m, p, wo, rng, q);
         if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
     }
     return cdivs(r, (float)16u);
