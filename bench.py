@@ -160,7 +160,7 @@ def main():
 
     cpu = None
     parity = None
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:  # the CPU baseline is timed at N=1 only
         # the reference library logs to stdout (base/Logger.cpp); keep stdout for the JSON line
         sys.stdout.flush()
         saved = os.dup(1)

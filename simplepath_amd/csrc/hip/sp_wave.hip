@@ -222,10 +222,19 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
     if (p >= w.pe) return;
     const PixelRef pr = pixel_of(sc, w, p);
     uint32_t       mask = 0, draws = 0;
+#ifdef SP_SHADE_PROF
+    // per-wave timeline of the stages (SP_WAVE_DIAG with a -DSP_SHADE_PROF build): the latest
+    // time any lane reached each point (s_memrealtime, 100 MHz)
+    uint64_t tp[6] = { __builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0 };
+#define SP_STAMP(k) (tp[k] = __builtin_amdgcn_s_memrealtime())
+#else
+#define SP_STAMP(k) ((void)0)
+#endif
     if (pr.inside) {
         const Rsq q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
         Rng       rng = rng_load(w, p);
         rng_prepare(rng);
+        SP_STAMP(1);
         const float4 hrec = w.hit[p];
         Hit          h;
         h.t     = hrec.x;
@@ -236,12 +245,15 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
             const Ray   ray = camera_ray(sc, pr, sample, q);
             const Isect is  = finish_hit(sc, h, ray, q);
             const f3    wo  = neg(ray.d);
+            SP_STAMP(2);
             for (int li = 0; li < sc.n_lights; ++li) {
                 const Light   l  = uload_light(sc.lights + li);
                 const LSample ls = light_sample(sc, l, is.p, is.n, next2D(rng), q);
+                SP_STAMP(3);
                 if (ls.pdf == 0.0f || cblack(ls.L)) continue;
                 const f3  wi = ls.ray.d;
                 const rgb f  = material_eval(sc, is.material, wo, wi, is.n, rng, q);
+                SP_STAMP(4);
                 if (cblack(f)) continue;
                 const rgb c = cdivs(cscale(cmul(f, ls.L), abs_f(dot(wi, is.n))), ls.pdf);
                 float4*   e = w.sh + ((size_t)li * w.n + p) * 2;
@@ -254,6 +266,21 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
         draws = rng.draws;
         rng_store(w, p, rng);
     }
+#ifdef SP_SHADE_PROF
+    SP_STAMP(5);
+    if (w.diag) {
+        for (int k = 1; k < 6; ++k) {
+            uint64_t v = tp[k];
+            for (int off = 32; off > 0; off >>= 1) v = max(v, (uint64_t)__shfl_xor((unsigned long long)v, off, 64));
+            tp[k] = v;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            unsigned long long* r = w.diag + (size_t)(p >> 6) * 8;
+            for (int k = 0; k < 6; ++k) r[k] = tp[k];
+        }
+    }
+#endif
+#undef SP_STAMP
     // Active-ray compaction: every (pixel, light) shadow ray becomes one queue item
     // (p << 5 | light).  Wave prefix sum of the per-lane counts, one atomic per wave on one of
     // QSEG segment counters (tile slot % QSEG) so that no single address serialises the chip.
@@ -613,13 +640,22 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     // shading instead of both parts shading at once.
     for (uint32_t i = 0; i < w.spp; ++i) {
         for (int k = 0; k < parts; ++k) {
+#ifdef SP_SHADE_PROF // the diag buffer holds the shade timeline only
+            const WaveArgs& wi = pd[k];
+            const WaveArgs& ws = (pw[k].diag && i == diag_sample) ? pw[k] : pd[k];
+#else
             const WaveArgs& wi = (pw[k].diag && i == diag_sample) ? pw[k] : pd[k];
+#endif
             hipStream_t     st = ps[k];
             if (sc.wide_closest) hipLaunchKernelGGL(wf_primary<true>, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
             else hipLaunchKernelGGL(wf_primary<false>, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
             if (k == 0) mark();
             if (parts > 1 && (k == 1 || i > 0)) (void)hipStreamWaitEvent(st, shade_done[1 - k], 0);
+#ifdef SP_SHADE_PROF
+            hipLaunchKernelGGL(shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, ws, i);
+#else
             hipLaunchKernelGGL(shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, pd[k], i);
+#endif
             if (parts > 1) (void)hipEventRecord(shade_done[k], st);
             if (k == 0) mark();
             if (dyn) hipLaunchKernelGGL(wf_shadow_dyn, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
