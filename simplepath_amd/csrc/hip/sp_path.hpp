@@ -474,7 +474,7 @@ struct WideHits {
     uint32_t child_base, leaf_base, meta_lo, meta_hi;
 };
 __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, const Ray& ray, const f3& inv, float tmin,
-                                               float tmax)
+                                               float tmax, uint32_t filter = 0xffu)
 {
     const uint4*   np = sc.wnodes + 5 * (size_t)node;
     const uint4    w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
@@ -492,6 +492,7 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
         const uint32_t meta  = ((k < 4 ? w1.z : w1.w) >> (8 * (k & 3))) & 0xffu;
         const bool     inner = (imask >> k) & 1u;
         if (!inner && meta == 0u) continue;
+        if (!((filter >> k) & 1u)) continue;
         const int   h  = k >> 2;
         const float lx = fma_f(ubyte(h ? w2.y : w2.x, k), sx, px);
         const float ly = fma_f(ubyte(h ? w2.w : w2.z, k), sy, py);
@@ -511,13 +512,18 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
     return r;
 }
 
+// Closest hit: the nearest internal child is visited next; the node is pushed with the mask
+// of its other hit internal children, and on pop it is visited again restricted to that mask --
+// the boxes are re-tested against the current t_max (culling) and the nearest survivor chosen,
+// so children are taken near-first with one stack entry per level (node << 8 | mask).
 __device__ __forceinline__ void wide_closest(const Scene& sc, const Ray& ray, float tmin, Hit& h, Stack st)
 {
-    const f3 inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp   = 0;
-    uint32_t node = 0;
+    const f3 inv    = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    int      sp     = 0;
+    uint32_t node   = 0;
+    uint32_t filter = 0xffu; // first visit: every child; revisit: pending internal children only
     while (true) {
-        const WideHits wh = wide_visit(sc, node, ray, inv, tmin, h.t);
+        const WideHits wh = wide_visit(sc, node, ray, inv, tmin, h.t, filter);
         for (uint32_t m = wh.leaf; m; m &= m - 1) {
             const int      k    = __ffs(m) - 1;
             const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
@@ -527,20 +533,18 @@ __device__ __forceinline__ void wide_closest(const Scene& sc, const Ray& ray, fl
         if (wh.inner) {
             const uint32_t rest = wh.inner & ~(1u << wh.nearest);
             if (rest) {
-                st.s[sp * 64 + st.lane] = (wh.child_base << 8) | rest;
+                st.s[sp * 64 + st.lane] = (node << 8) | rest;
                 ++sp;
             }
-            node = wh.child_base + (uint32_t)wh.nearest;
+            node   = wh.child_base + (uint32_t)wh.nearest;
+            filter = 0xffu;
             continue;
         }
         if (sp == 0) break;
-        const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
-        uint32_t       m = e & 0xffu;
-        const int      k = __ffs(m) - 1;
-        m &= m - 1;
-        if (m) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | m;
-        else --sp;
-        node = (e >> 8) + (uint32_t)k;
+        --sp;
+        const uint32_t e = st.s[sp * 64 + st.lane];
+        node             = e >> 8;
+        filter           = e & 0xffu;
     }
 }
 
