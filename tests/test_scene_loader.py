@@ -49,3 +49,74 @@ def test_set_resolution_rebuilds_camera(scene_dir):
     b = s.desc().camera.transform
     assert s.width == 1920 and s.height == 1080
     assert list(b.vz) != vz0
+
+
+def _env_scene(tmp_path, pixels, extra="", radiance="1.0 1.0 1.0", name="env.pfm"):
+    scenes.write_pfm(str(tmp_path / name), pixels)
+    text = ("version: 1\nperspective_camera {\n origin: 0 0 1\n look_at: 0 0 0\n}\n"
+            f'environment_light {{\n radiance: {radiance}\n image: "{name}"\n{extra}}}\n')
+    return sp.Scene.from_string(text, str(tmp_path))
+
+
+def test_image_environment_light_desc(tmp_path):
+    # Image/Image.cpp read_pfm (rows bottom-up in the file) then img *= radiance (FileParser.cpp:367)
+    rng = np.random.default_rng(3)
+    img = rng.uniform(0.0, 4.0, (6, 10, 3)).astype(np.float32)
+    s = _env_scene(tmp_path, img, extra=" max_radiance: 2.5\n rotate: 0 1 0 45\n", radiance="2.0 1.0 0.5")
+    d = s.desc()
+    assert d.info.num_lights == 1 and d.num_env_images == 1
+    assert d.lights[0].kind == 2 and d.lights[0].image == 0  # SP_LIGHT_IMAGE_ENVIRONMENT
+    e = d.env_images[0]
+    assert (e.width, e.height) == (10, 6)
+    assert e.max_radiance == np.float32(2.5)
+    px = np.ctypeslib.as_array(e.pixels, shape=(6, 10, 3))
+    assert np.array_equal(px, img * np.array([2.0, 1.0, 0.5], dtype=np.float32))
+    l2w = np.array([list(e.light_to_world.vx), list(e.light_to_world.vy), list(e.light_to_world.vz)])
+    w2l = np.array([list(e.world_to_light.vx), list(e.world_to_light.vy), list(e.world_to_light.vz)])
+    assert np.allclose(l2w.T @ w2l.T, np.eye(3), atol=1e-6)  # inverse pair
+    assert abs(l2w[0][0] - np.cos(np.pi / 4)) < 1e-6
+
+
+def test_image_environment_light_defaults_and_errors(tmp_path):
+    img = np.ones((2, 4, 3), dtype=np.float32)
+    s = _env_scene(tmp_path, img)  # the desc points into the scene: keep it alive
+    d = s.desc()
+    assert d.env_images[0].max_radiance == np.float32(np.finfo(np.float32).max)  # numeric_limits<float>::max()
+    cam = "perspective_camera {\n origin: 0 0 1\n look_at: 0 0 0\n}\n"
+    with pytest.raises(sp.SimplePathError) as e:  # unable to open -> reference's ImageError
+        sp.Scene.from_string('version: 1\n' + cam + 'environment_light {\n image: "missing.pfm"\n}\n', str(tmp_path))
+    assert "Unable to open" in str(e.value)
+    (tmp_path / "bad.pfm").write_bytes(b"P6\n1 1\n255\n\x00\x00\x00")
+    with pytest.raises(sp.SimplePathError) as e:
+        sp.Scene.from_string('version: 1\n' + cam + 'environment_light {\n image: "bad.pfm"\n}\n', str(tmp_path))
+    assert "Unexpected format" in str(e.value)
+
+
+def test_big_endian_pfm(tmp_path):
+    img = np.arange(2 * 3 * 3, dtype=np.float32).reshape(2, 3, 3)
+    with open(tmp_path / "be.pfm", "wb") as fh:
+        fh.write(b"PF\n3 2\n1.0\n")
+        fh.write(np.ascontiguousarray(img[::-1].astype(">f4")).tobytes())
+    cam = "perspective_camera {\n origin: 0 0 1\n look_at: 0 0 0\n}\n"
+    s = sp.Scene.from_string('version: 1\n' + cam + 'environment_light {\n image: "be.pfm"\n}\n', str(tmp_path))
+    d = s.desc()
+    assert np.array_equal(np.ctypeslib.as_array(d.env_images[0].pixels, shape=(2, 3, 3)), img)
+
+
+def test_stl_mesh_welding(scene_dir):
+    # binary STL: vertices welded (std::map<Point3>), one shared vertex set for the closed surface
+    s = sp.Scene.from_file(os.path.join(scene_dir, "elf_small.sp"))
+    i = s.info()
+    v, f = scenes.elf_mesh(24)
+    assert i.num_triangles == f.shape[0]
+    assert i.num_vertices == v.shape[0]
+    assert i.max_depth == 16
+
+
+def test_ascii_stl_unsupported(tmp_path):
+    (tmp_path / "a.stl").write_text("solid x\nendsolid x\n")
+    with pytest.raises(sp.SimplePathError) as e:
+        sp.Scene.from_string('version: 1\nperspective_camera {\n origin: 0 0 1\n look_at: 0 0 0\n}\n'
+                             'material_lambertian {\n name: "m"\n diffuse: 1 1 1\n}\n'
+                             'mesh {\n file: "a.stl"\n material: "m"\n}\n', str(tmp_path))
+    assert "ASCII STL" in str(e.value)
