@@ -676,7 +676,16 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
         up(m.cond_int, &x.cond_int);
         up(m.marg_func, &x.marg_func);
         up(m.marg_cdf, &x.marg_cdf);
-        x.marg_int = m.marg_int;
+        x.marg_int   = m.marg_int;
+        x.cond_guide = nullptr;
+        x.marg_guide = nullptr;
+        x.cond_bits  = m.cond_bits;
+        x.marg_bits  = m.marg_bits;
+        const char* ge = std::getenv("SP_ENV_GUIDE"); // 0: replay the exact upper_bound (comparison)
+        if (m.guided && !(ge && std::atoi(ge) == 0)) {
+            up(m.cond_guide, &x.cond_guide);
+            up(m.marg_guide, &x.marg_guide);
+        }
         envs.push_back(x);
     }
     d.envs = nullptr;

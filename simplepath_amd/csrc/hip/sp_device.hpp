@@ -61,6 +61,9 @@ struct EnvMap {
     const float*    marg_func; // nv
     const float*    marg_cdf;  // nv + 1
     float           marg_int;
+    const uint32_t* cond_guide; // nv x (2^cond_bits + 1); nullptr: exact upper_bound replay
+    const uint32_t* marg_guide; // 2^marg_bits + 1
+    int32_t         cond_bits, marg_bits;
 };
 
 struct Material {

@@ -849,10 +849,26 @@ __device__ __forceinline__ int dist_offset(const float* cdf, int n, float u)
     }
     return (first >= n) ? n - 1 : first; // it == end() || it == prev(end())
 }
-// Distribution1D::sample_continuous (math/Distribution1D.h:72) on [0, 1]
-__device__ __forceinline__ float dist_sample(const float* func, const float* cdf, int n, float integral, float u, float& pdf, int& off)
+// The same offset through a guide table (sp_host.hpp EnvMap): cdf[0..n-1] is non-decreasing, so
+// the replayed search returns the first i < n with u < cdf[i] (else n - 1); the guide narrows it
+// to [guide[b], guide[b+1]] for b = floor(u * 2^bits) (exact: power-of-two scale), usually one
+// or two entries, instead of 13 dependent probes over a 32 KB row.
+__device__ __forceinline__ int dist_offset_guided(const float* cdf, const uint32_t* guide, int bits, float u)
 {
-    off            = dist_offset(cdf, n, u);
+    const int b  = (int)(u * (float)(1 << bits));
+    int       lo = (int)guide[b], hi = (int)guide[b + 1];
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (u < cdf[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+// Distribution1D::sample_continuous (math/Distribution1D.h:72) on [0, 1]
+__device__ __forceinline__ float dist_sample(const float* func, const float* cdf, int n, float integral, float u, float& pdf,
+                                             int& off, const uint32_t* guide = nullptr, int bits = 0)
+{
+    off            = guide ? dist_offset_guided(cdf, guide, bits, u) : dist_offset(cdf, n, u);
     const float c0 = cdf[off], c1 = cdf[off + 1];
     float       du = u - c0;
     if ((c1 - c0) > 0.0f) du /= (c1 - c0);
@@ -904,8 +920,10 @@ __device__ __forceinline__ EnvSample env_sample(const EnvMap& e, P2 u)
     EnvSample s;
     float     pdf1, pdf0;
     int       v, iu;
-    const float d1 = dist_sample(e.marg_func, e.marg_cdf, e.nv, e.marg_int, u.y, pdf1, v);
-    const float d0 = dist_sample(e.cond_func + (size_t)v * e.nu, e.cond_cdf + (size_t)v * (e.nu + 1), e.nu, e.cond_int[v], u.x, pdf0, iu);
+    const float d1 = dist_sample(e.marg_func, e.marg_cdf, e.nv, e.marg_int, u.y, pdf1, v, e.marg_guide, e.marg_bits);
+    const uint32_t* cg = e.cond_guide ? e.cond_guide + (size_t)v * ((1u << e.cond_bits) + 1u) : nullptr;
+    const float d0 = dist_sample(e.cond_func + (size_t)v * e.nu, e.cond_cdf + (size_t)v * (e.nu + 1), e.nu, e.cond_int[v], u.x,
+                                 pdf0, iu, cg, e.cond_bits);
     const float map_pdf = pdf0 * pdf1;
     if (map_pdf == 0.0f) {
         s.L   = mkc(0, 0, 0);

@@ -8,6 +8,7 @@
 // same texel and pdf bits as the reference.
 #include "sp_host.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -81,6 +82,27 @@ void distribution_1d(const float* f_in, size_t n, float* func, float* cdf, float
     }
 }
 
+// guide table (sp_host.hpp EnvMap): returns false if cdf[0..n-1] is not non-decreasing
+bool build_guide(const float* cdf, size_t n, int bits, uint32_t* guide)
+{
+    for (size_t i = 1; i < n; ++i)
+        if (!(cdf[i - 1] <= cdf[i])) return false;
+    const size_t G = (size_t)1 << bits;
+    size_t       i = 0;
+    for (size_t b = 0; b <= G; ++b) {
+        const float v = std::ldexp((float)b, -bits); // exact: b / 2^bits
+        while (i < n && !(cdf[i] > v)) ++i;
+        guide[b] = (uint32_t)std::min(i, n - 1);
+    }
+    return true;
+}
+int guide_bits(size_t n)
+{
+    int b = 0;
+    while (((size_t)1 << b) < n && b < 16) ++b;
+    return b;
+}
+
 } // namespace
 
 EnvMap build_env_map(const EnvImage& img)
@@ -129,6 +151,15 @@ EnvMap build_env_map(const EnvImage& img)
     m.marg_func.resize((size_t)height);
     m.marg_cdf.resize((size_t)height + 1);
     distribution_1d(m.cond_int.data(), (size_t)height, m.marg_func.data(), m.marg_cdf.data(), &m.marg_int);
+    m.cond_bits = guide_bits((size_t)width);
+    m.marg_bits = guide_bits((size_t)height);
+    const size_t cg = ((size_t)1 << m.cond_bits) + 1;
+    m.cond_guide.resize(cg * (size_t)height);
+    m.marg_guide.resize(((size_t)1 << m.marg_bits) + 1);
+    m.guided = build_guide(m.marg_cdf.data(), (size_t)height, m.marg_bits, m.marg_guide.data());
+    for (int v = 0; v < height && m.guided; ++v)
+        m.guided = build_guide(&m.cond_cdf[(size_t)v * (width + 1)], (size_t)width, m.cond_bits, &m.cond_guide[(size_t)v * cg]);
+    if (!m.guided) { m.cond_guide.clear(); m.marg_guide.clear(); }
     return m;
 }
 

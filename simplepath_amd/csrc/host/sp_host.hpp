@@ -79,6 +79,14 @@ struct EnvMap {
     std::vector<float> cond_int;              // nv        m_function_integral
     std::vector<float> marg_func, marg_cdf;   // nv, nv + 1
     float              marg_int = 0.0f;
+    // Guide tables for Distribution1D::get_offset: cdf[0..n-1] is non-decreasing (only cdf[n],
+    // the integral, breaks the order), so the libstdc++ upper_bound result equals "first i < n
+    // with u < cdf[i], else n - 1".  guide[b] = that index for u = b / 2^bits (first i with
+    // cdf[i] > b / 2^bits, clamped to n - 1): u in [b, b+1) / 2^bits lies in [guide[b], guide[b+1]].
+    bool                  guided = false;     // false: some row is not ordered (NaN texels)
+    int                   cond_bits = 0, marg_bits = 0;
+    std::vector<uint32_t> cond_guide;         // nv x (2^cond_bits + 1)
+    std::vector<uint32_t> marg_guide;         // 2^marg_bits + 1
 };
 EnvMap build_env_map(const EnvImage& img);
 // Image/Image.cpp:78 read_pfm: img(x, y), rows stored bottom-up in the file.

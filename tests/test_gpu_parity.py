@@ -93,8 +93,11 @@ def test_vs_glibc_oracle_bitexact(scene_dir, integrator):
 
 @pytest.mark.parametrize("integrator", ["direct_lighting", "brute_force_iterative_rr", "iterative_rrnee", "whitted",
                                         "brute_force"])
-def test_image_environment_light_bitexact(scene_dir, integrator):
-    # ImageBasedEnvironmentLight: Distribution2D sampling, MIS pdf, escaping-ray lookups
+@pytest.mark.parametrize("guide", ["1", "0"])
+def test_image_environment_light_bitexact(scene_dir, monkeypatch, integrator, guide):
+    # ImageBasedEnvironmentLight: Distribution2D sampling (guide tables, or the replayed libstdc++
+    # upper_bound with SP_ENV_GUIDE=0), MIS pdf, escaping-ray lookups
+    monkeypatch.setenv("SP_ENV_GUIDE", guide)
     s = load(scene_dir, "material_spheres_ibl.sp", 24, 48, bvh=1)
     g, gst = sp.render_tiles(s, integrator, 4)
     c, cst = _oracle.render(s, sp.string_to_integrator_type(integrator), 4, variant="glibc")
