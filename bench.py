@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront"])
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
     a = ap.parse_args()
     sc = SCENES[a.scene]
@@ -110,6 +112,9 @@ def main():
     n_tiles = sched.get_num_tiles()
     my_tiles = shard.shard_tiles(n_tiles, rank, world)
     per_rank = shard.per_rank_capacity(n_tiles, world)
+    if args.sim_world > 1 and world == 1:
+        my_tiles = shard.shard_tiles(n_tiles, 0, args.sim_world)
+        per_rank = shard.per_rank_capacity(n_tiles, args.sim_world)
     out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
     gathered, frame = None, None
     if dist is not None and rank == 0:

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +18,8 @@ namespace spd {
 hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
+hipError_t launch_tile_cost(const Scene& sc, const int32_t* tile_ids, int64_t n_tiles, int32_t tiles_x, float* cost,
+                            hipStream_t stream);
 } // namespace spd
 
 namespace {
@@ -228,6 +231,9 @@ struct sp_scene {
     hipEvent_t           ev_shade[2] = { nullptr, nullptr };
     int                  n_cu         = 0;
     hipEvent_t           ev0 = nullptr, ev1 = nullptr;
+    float*               d_cost     = nullptr; // megakernel tile order (longest first)
+    int32_t*             d_order    = nullptr;
+    size_t               order_cap  = 0;
     void*                deep_buf   = nullptr; // recursive integrators beyond MAX_RECURSION levels
     size_t               deep_cap   = 0;
     // multi-bounce wavefront (sp_wpath.hip)
@@ -264,6 +270,9 @@ struct sp_scene {
         if (ev1) (void)hipEventDestroy(ev1);
         if (wp_buf) (void)hipFree(wp_buf);
         if (deep_buf) (void)hipFree(deep_buf);
+        if (d_cost) (void)hipFree(d_cost);
+        if (d_order) (void)hipFree(d_order);
+        d_cost = nullptr; d_order = nullptr; order_cap = 0;
         deep_buf = nullptr; deep_cap = 0;
         if (wp_ctl) (void)hipFree(wp_ctl);
         if (wp_host) (void)hipHostFree(wp_host);
@@ -765,7 +774,14 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
                                         "BruteForceIterative(RR) and IterativeRRNEE");
     // AUTO: the split pipeline where it wins -- DirectLighting; the iterative integrators run the
     // regenerating megakernel (sp_mega.hpp), which measured faster than sp_wpath
-    if (pipeline == SP_PIPELINE_AUTO) pipeline = wave_ok ? SP_PIPELINE_WAVEFRONT : SP_PIPELINE_MEGAKERNEL;
+    // DirectLighting: the wavefront needs many pixels in flight -- every launch waits for its
+    // slowest wave, once per sample.  Below SP_WAVE_MIN_TILES tiles (default 24000: between
+    // the 1-GPU frame, 32400 tiles, and its 2-GPU shard, 16200) the persistent megakernel,
+    // with its tiles taken longest-first, is faster.
+    int64_t wave_min = 24000;
+    if (const char* v = std::getenv("SP_WAVE_MIN_TILES")) wave_min = std::atoll(v);
+    if (pipeline == SP_PIPELINE_AUTO)
+        pipeline = (wave_ok && n_tiles >= wave_min) ? SP_PIPELINE_WAVEFRONT : SP_PIPELINE_MEGAKERNEL;
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
     int launches = 0, parts_used = 1;
     if (pipeline == SP_PIPELINE_WAVEFRONT && wpath_ok) {
@@ -970,9 +986,53 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
             a.deep        = static_cast<float*>(s->deep_buf);
             a.deep_stride = lanes;
         }
+        // SP_TILE_ORDER=1: longest-first tile order (a probe of one centre ray per pixel ranks the
+        // tiles; probe and sort are inside the timed render).  Opt-in: measured slower than the
+        // scheduler's own order on bunny at 2-8 GPUs' shards -- the frame's end is
+        // set by the slowest single tile, which no order shortens.
+        a.order = nullptr;
         SP_HIP(hipEventRecord(s->ev0, stream));
+        bool order_on = false;
+        if (const char* v = std::getenv("SP_TILE_ORDER")) order_on = std::atoi(v) != 0 && n_tiles > 1;
+        if (order_on) {
+            if ((size_t)n_tiles > s->order_cap) {
+                if (s->d_cost) (void)hipFree(s->d_cost);
+                if (s->d_order) (void)hipFree(s->d_order);
+                s->d_cost = nullptr; s->d_order = nullptr; s->order_cap = 0;
+                SP_HIP(hipMalloc(&s->d_cost, (size_t)n_tiles * sizeof(float)));
+                SP_HIP(hipMalloc(&s->d_order, (size_t)n_tiles * sizeof(int32_t)));
+                s->order_cap = (size_t)n_tiles;
+            }
+            SP_HIP(spd::launch_tile_cost(s->dev, a.tile_ids, n_tiles, a.tiles_x, s->d_cost, stream));
+            std::vector<float> cost((size_t)n_tiles);
+            SP_HIP(hipMemcpyAsync(cost.data(), s->d_cost, cost.size() * sizeof(float), hipMemcpyDeviceToHost, stream));
+            SP_HIP(hipStreamSynchronize(stream));
+            std::vector<int32_t> order((size_t)n_tiles);
+            for (size_t i = 0; i < order.size(); ++i) order[i] = (int32_t)i;
+            std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cost[(size_t)x] > cost[(size_t)y]; });
+            SP_HIP(hipMemcpyAsync(s->d_order, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+            a.order = s->d_order;
+        }
+        // SP_TILE_DIAG=<file>: per-tile timeline {t0, t1, wave, item} (u64, s_memrealtime 100 MHz)
+        const char*         tdiag_path = std::getenv("SP_TILE_DIAG");
+        unsigned long long* tdiag      = nullptr;
+        if (tdiag_path) {
+            SP_HIP(hipMalloc(&tdiag, (size_t)n_tiles * 4 * sizeof(unsigned long long)));
+            SP_HIP(hipMemsetAsync(tdiag, 0, (size_t)n_tiles * 4 * sizeof(unsigned long long), stream));
+        }
+        a.tile_diag = tdiag;
         SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
-        launches = 1;
+        SP_HIP(hipStreamSynchronize(stream)); // the order vector above must outlive the async copy
+        if (tdiag) {
+            std::vector<unsigned long long> rec((size_t)n_tiles * 4);
+            SP_HIP(hipMemcpy(rec.data(), tdiag, rec.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            (void)hipFree(tdiag);
+            if (FILE* f = std::fopen(tdiag_path, "wb")) {
+                std::fwrite(rec.data(), sizeof(unsigned long long), rec.size(), f);
+                std::fclose(f);
+            }
+        }
+        launches = order_on ? 2 : 1;
     }
     SP_HIP(hipEventRecord(s->ev1, stream));
     SP_HIP(hipEventSynchronize(s->ev1));

@@ -48,8 +48,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
     while (true) {
         int grabbed = 0;
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
-        const int64_t slot = __shfl(grabbed, 0, 64);
-        if (slot >= args.num_tiles) break;
+        const int64_t item = __shfl(grabbed, 0, 64);
+        if (item >= args.num_tiles) break;
+        const int64_t slot = args.order ? args.order[item] : item; // longest-first order, if given
+        const uint64_t t_start = args.tile_diag ? __builtin_amdgcn_s_memrealtime() : 0;
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
         const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
         const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
@@ -90,6 +92,11 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         o[0]     = acc.r;
         o[1]     = acc.g;
         o[2]     = acc.b;
+        if (args.tile_diag && lane < 4) {
+            const uint64_t t_end  = __builtin_amdgcn_s_memrealtime();
+            const uint64_t rec[4] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item };
+            args.tile_diag[(size_t)slot * 4 + lane] = rec[lane];
+        }
     }
     unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
     for (int k = 0; k < 4; ++k) {
@@ -178,8 +185,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_regen(Sc
     while (true) {
         int grabbed = 0;
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
-        const int64_t slot = __shfl(grabbed, 0, 64);
-        if (slot >= args.num_tiles) break;
+        const int64_t item = __shfl(grabbed, 0, 64);
+        if (item >= args.num_tiles) break;
+        const int64_t slot = args.order ? args.order[item] : item; // longest-first order, if given
+        const uint64_t t_start = args.tile_diag ? __builtin_amdgcn_s_memrealtime() : 0;
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
         const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
         const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
@@ -230,6 +239,11 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_regen(Sc
         o[0]     = acc.r;
         o[1]     = acc.g;
         o[2]     = acc.b;
+        if (args.tile_diag && lane < 4) {
+            const uint64_t t_end  = __builtin_amdgcn_s_memrealtime();
+            const uint64_t rec[4] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item };
+            args.tile_diag[(size_t)slot * 4 + lane] = rec[lane];
+        }
     }
     unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
     for (int k = 0; k < 4; ++k) {

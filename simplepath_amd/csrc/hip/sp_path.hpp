@@ -33,12 +33,22 @@ __device__ __forceinline__ float rsqrt_ref(float a, const Rsq& q)
 }
 __device__ __forceinline__ f3 normalize(f3 a, const Rsq& q) { return scale(a, rsqrt_ref(dot(a, a), q)); }
 
+// Draw-ahead window: the next RNG_PF words of the current generation are loaded RNG_PF draws
+// before they are consumed, so a draw does not wait for a global load (the state lives in HBM,
+// 160 KB per wave).  The window never crosses into the other buffer and is emptied at every
+// buffer switch, so the stream is the same word sequence as without it.
+#ifndef SP_RNG_PF
+#define SP_RNG_PF 2
+#endif
+constexpr int RNG_PF = SP_RNG_PF;
 struct Rng {
     uint64_t* base;  // lane-offset base of this wave slot's state, stride 64 words
     int       cur;   // generation buffer being consumed
     int       idx;   // next word in it
     int       ready; // other buffer already holds the next generation
     uint32_t  draws;
+    int       pfn = 0;        // valid words in pf (words idx .. idx + pfn - 1 of buffer cur)
+    uint64_t  pf[RNG_PF > 0 ? RNG_PF : 1];
 };
 
 __device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_N * 64; }
@@ -75,6 +85,7 @@ __device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
     r.idx   = MT_N; // std::mt19937_64 starts with _M_p = n: first draw twists
     r.ready = 0;
     r.draws = 0;
+    r.pfn   = 0;
 }
 
 // Twist ahead at a wave-synchronous point (sample / bounce start).  A lane may compute its next
@@ -101,9 +112,26 @@ __device__ __forceinline__ uint64_t rng_raw(Rng& r)
         r.cur ^= 1;
         r.idx   = 0;
         r.ready = 0;
+        r.pfn   = 0;
     }
-    const uint64_t w = mt_buf(r, r.cur)[(size_t)r.idx * 64];
+    const uint64_t* b = mt_buf(r, r.cur);
+    uint64_t        w;
+    if (RNG_PF > 0 && r.pfn > 0) {
+        w = r.pf[0];
+#pragma unroll
+        for (int k = 0; k + 1 < RNG_PF; ++k) r.pf[k] = r.pf[k + 1];
+        --r.pfn;
+    } else {
+        w = b[(size_t)r.idx * 64];
+    }
     ++r.idx;
+    // top the window up to RNG_PF words ahead (static indices: the window stays in registers)
+#pragma unroll
+    for (int k = 0; k < RNG_PF; ++k)
+        if (r.pfn == k && r.idx + k < MT_N) {
+            r.pf[k] = b[(size_t)(r.idx + k) * 64];
+            r.pfn   = k + 1;
+        }
     ++r.draws;
     return mt_temper(w);
 }

@@ -26,6 +26,9 @@
 //   acc[3][n] f32 SoA | rstate[n] u32 {idx | cur<<16 | ready<<17} | hit[n] float4 {t, code,
 //   beta, gamma} | shp[n] float4 {p.xyz, light mask} | sh[light][n][2] float4 {wi.xyz, tmin},
 //   {contrib.rgb, tmax} | queue[n] u32 | mt[tile][buf][312][64] u64 (as in the megakernel).
+// RNG draw-ahead window (sp_path.hpp Rng): off in the wavefront kernels, where it measured
+// 1-2 % slower (it pays off in the megakernel, 2 words ahead).
+#define SP_RNG_PF 0
 #include "sp_packet.hpp"
 #include "sp_wave.hpp"
 

@@ -105,6 +105,20 @@ def test_image_environment_light_bitexact(scene_dir, monkeypatch, integrator, gu
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), (integrator, rel_l2(g, c))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["bunny.sp", "material_spheres_ibl.sp"])
+def test_tile_order_is_invisible(scene_dir, scene, monkeypatch):
+    # longest-first tile order only changes which wave takes which tile, never a pixel's bits
+    s = load(scene_dir, scene, 72, 40, bvh=0)
+    monkeypatch.setenv("SP_TILE_ORDER", "1")
+    a, ast = sp.render_tiles(s, "direct_lighting", 3, pipeline="megakernel")
+    monkeypatch.setenv("SP_TILE_ORDER", "0")
+    b, bst = sp.render_tiles(s, "direct_lighting", 3, pipeline="megakernel")
+    assert ast.launches == 2 and bst.launches == 1
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (ast.rays, ast.shadow_rays, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.rng_draws)
+
+
 @pytest.mark.parametrize("scene,bvh", [("bunny.sp", 0), ("material_spheres.sp", 1), ("material_spheres_ibl.sp", 0)])
 def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
     # the two device pipelines run the same floating-point sequence per pixel
