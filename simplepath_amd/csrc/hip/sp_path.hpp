@@ -93,7 +93,10 @@ __device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
 // twist together -- but only once some lane is within RNG_MARGIN draws of exhausting its buffer.
 // Twists are thus batched (about one per 312 draws per wave instead of one per sample), and the
 // in-draw fallback (rng_raw) keeps the stream exact when a path draws more than the margin.
-constexpr int RNG_MARGIN = 96;
+#ifndef SP_RNG_MARGIN
+#define SP_RNG_MARGIN 96
+#endif
+constexpr int RNG_MARGIN = SP_RNG_MARGIN;
 __device__ __forceinline__ void rng_prepare(Rng& r)
 {
     const bool urgent = !r.ready && r.idx >= MT_N - RNG_MARGIN;
@@ -1434,18 +1437,25 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     float       c        = p.c0;
     const float sample_x = std_max(U1, 1e-6f);
     float       b        = c - (1.0f + c) * lm_powf(1.0f - sample_x, p.fit);
+    // erfinv(b) at the converged b is the last iteration's inv_erf (same b, same function), so
+    // the final erfinv is only evaluated when the loop ran out of iterations (b moved after it)
+    float inv_erf   = 0.0f;
+    bool  converged = false;
     for (int it = 0; it < 9; ++it) {
         if (!(b >= a && b <= c)) b = 0.5f * (a + c);
-        const float inv_erf = erfinv(b);
+        inv_erf = erfinv(b);
         const float value =
             p.normalization * (1.0f + b + p.sqrt_pi_inv * p.tan_theta_i * lm_expf(-inv_erf * inv_erf)) - sample_x;
         const float derivative = p.normalization * (1.0f - inv_erf * p.tan_theta_i);
-        if (abs_f(value) < 1e-5f) break;
+        if (abs_f(value) < 1e-5f) {
+            converged = true;
+            break;
+        }
         if (value > 0) c = b;
         else a = b;
         b -= value / derivative;
     }
-    s.x = erfinv(b);
+    s.x = converged ? inv_erf : erfinv(b);
     s.y = erfinv(2.0f * std_max(U2, 1e-6f) - 1.0f);
     return s;
 }
