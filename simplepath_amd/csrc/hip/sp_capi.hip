@@ -491,7 +491,7 @@ float sp_host_rsqrt_emulated(float x)
     return spm::rsqrtss_emulated(x, t);
 }
 
-int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
+static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
 {
     if (!s) return fail(SP_ERR_ARG, "null scene");
     if (bvh_mode != 0 && bvh_mode != 1) return fail(SP_ERR_ARG, "bvh_mode must be 0 (SAH) or 1 (reference)");
@@ -553,7 +553,11 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     }
     std::vector<int32_t> unbounded;
     for (size_t i = part; i < prims.size(); ++i) unbounded.push_back(h.prim_index[prims[i]]);
-    const sph::Bvh bvh = (bvh_mode == 1) ? sph::build_bvh_reference(bounds) : sph::build_bvh_sah(bounds, 4);
+    // SAH leaf size limit (SP_SAH_LEAF tuning knob, 1..4: 8 collapsed leaves of a wide node must
+    // fit its 5-bit leaf offsets; the sweep in DESIGN.md §4 found 4 best)
+    int sah_leaf = 4;
+    if (const char* v = std::getenv("SP_SAH_LEAF")) sah_leaf = std::max(1, std::min(4, std::atoi(v)));
+    const sph::Bvh bvh = (bvh_mode == 1) ? sph::build_bvh_reference(bounds) : sph::build_bvh_sah(bounds, sah_leaf);
     std::vector<float4>   slot_tri(bvh.prim_order.size() * 3);
     std::vector<uint32_t> slot_code(bvh.prim_order.size());
     for (size_t sl = 0; sl < bvh.prim_order.size(); ++sl) {
@@ -729,7 +733,32 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
     return SP_OK;
 }
 
+// No C++ exception crosses the C ABI: host-side failures (allocation, BVH encoding limits)
+// come back as error codes with sp_last_error() set.
+int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
+{
+    try {
+        return scene_upload_impl(s, device, bvh_mode);
+    } catch (const sph::SpError& e) {
+        return fail(e.code, e.what());
+    } catch (const std::exception& e) {
+        return fail(SP_ERR_UNSUPPORTED, std::string("scene upload failed: ") + e.what());
+    }
+}
+
+static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats);
 int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats)
+{
+    try {
+        return render_tiles_impl(s, p, d_out, stats);
+    } catch (const sph::SpError& e) {
+        return fail(e.code, e.what());
+    } catch (const std::exception& e) {
+        return fail(SP_ERR_HIP, std::string("render failed: ") + e.what());
+    }
+}
+
+static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats)
 {
     if (!s || !p || !d_out) return fail(SP_ERR_ARG, "null argument");
     if (s->device < 0) return fail(SP_ERR_STATE, "sp_scene_upload must be called before sp_render_tiles");

@@ -7,6 +7,8 @@
 // SAH (Wald 2007) with the same node format; it changes only the visiting order.
 #include "sp_host.hpp"
 
+#include <cstdlib>
+
 #include <stdexcept>
 #include <cstring>
 
@@ -104,6 +106,7 @@ struct SahBuilder {
     std::vector<float>             cx, cy, cz;
     std::vector<BvhNode>           nodes;
     int                            max_leaf;
+    float                          trav_cost = 1.0f; // node visit cost in triangle tests
     int                            max_depth = 0;
 
     static float area(const Box& b)
@@ -182,7 +185,7 @@ struct SahBuilder {
         }
         const float leaf_cost = area(bb) * static_cast<float>(n);
         // traversal cost ~ 1 triangle test per node visit; stop when the split does not pay
-        if (best_dim < 0 || (n <= static_cast<size_t>(max_leaf) && best_cost + area(bb) >= leaf_cost)) {
+        if (best_dim < 0 || (n <= static_cast<size_t>(max_leaf) && best_cost + trav_cost * area(bb) >= leaf_cost)) {
             if (best_dim < 0 && n > static_cast<size_t>(max_leaf)) {
                 // all centroids coincide: median split by index
                 const size_t mid = first + n / 2;
@@ -220,6 +223,7 @@ Bvh build_bvh_sah(const std::vector<PrimBounds>& bounds, int max_leaf)
 {
     Bvh        out;
     SahBuilder b{ bounds, {}, {}, {}, {}, {}, max_leaf };
+    if (const char* v = std::getenv("SP_SAH_CT")) b.trav_cost = (float)std::atof(v); // tuning knob
     const size_t n = bounds.size();
     b.ids.resize(n);
     b.cx.resize(n); b.cy.resize(n); b.cz.resize(n);
