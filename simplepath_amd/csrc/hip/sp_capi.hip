@@ -1042,18 +1042,19 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             SP_HIP(hipMemcpyAsync(s->d_order, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice, stream));
             a.order = s->d_order;
         }
-        // SP_TILE_DIAG=<file>: per-tile timeline {t0, t1, wave, item} (u64, s_memrealtime 100 MHz)
+        // SP_TILE_DIAG=<file>: per-tile timeline {t0, t1, wave, item} (u64, s_memrealtime 100 MHz) and,
+        // in a -DSP_MEGA_PROF build, shader clocks in trace / light sample / eval / occlusion
         const char*         tdiag_path = std::getenv("SP_TILE_DIAG");
         unsigned long long* tdiag      = nullptr;
         if (tdiag_path) {
-            SP_HIP(hipMalloc(&tdiag, (size_t)n_tiles * 4 * sizeof(unsigned long long)));
-            SP_HIP(hipMemsetAsync(tdiag, 0, (size_t)n_tiles * 4 * sizeof(unsigned long long), stream));
+            SP_HIP(hipMalloc(&tdiag, (size_t)n_tiles * 8 * sizeof(unsigned long long)));
+            SP_HIP(hipMemsetAsync(tdiag, 0, (size_t)n_tiles * 8 * sizeof(unsigned long long), stream));
         }
         a.tile_diag = tdiag;
         SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
         SP_HIP(hipStreamSynchronize(stream)); // the order vector above must outlive the async copy
         if (tdiag) {
-            std::vector<unsigned long long> rec((size_t)n_tiles * 4);
+            std::vector<unsigned long long> rec((size_t)n_tiles * 8);
             SP_HIP(hipMemcpy(rec.data(), tdiag, rec.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
             (void)hipFree(tdiag);
             if (FILE* f = std::fopen(tdiag_path, "wb")) {

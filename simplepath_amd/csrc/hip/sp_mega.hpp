@@ -57,6 +57,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
         const bool     inside = (int)px < sc.width && (int)py < sc.height;
         rgb            acc    = mkc(0, 0, 0);
+        uint64_t       prof[4] = { 0, 0, 0, 0 };
         if (inside) {
             const uint32_t pix_seed = (px << 16u) | py;
             rng_seed(rng, pix_seed ^ 0xb0ae9d99u);          // get_integrator_sampler (main.cpp:73)
@@ -83,6 +84,9 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
                     acc = cadd(acc, integrate<INTEG>(c, ray)); // image(p) += integrate(...)
             }
             acc = cdivs(acc, (float)args.spp); // image(p) /= num_pixel_samples
+#ifdef SP_MEGA_PROF
+            for (int k = 0; k < 4; ++k) prof[k] = c.prof[k];
+#endif
             rays_total += c.rays;
             shadow_total += c.shadow;
             samples_total += args.spp;
@@ -92,10 +96,16 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         o[0]     = acc.r;
         o[1]     = acc.g;
         o[2]     = acc.b;
-        if (args.tile_diag && lane < 4) {
+        if (args.tile_diag) {
+            // {t0, t1, wave, item, then per stage the largest shader-clock total of any lane}
+            for (int k = 0; k < 4; ++k)
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(prof[k], off, 64);
+                    prof[k]          = o > prof[k] ? o : prof[k];
+                }
             const uint64_t t_end  = __builtin_amdgcn_s_memrealtime();
-            const uint64_t rec[4] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item };
-            args.tile_diag[(size_t)slot * 4 + lane] = rec[lane];
+            const uint64_t rec[8] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item, prof[0], prof[1], prof[2], prof[3] };
+            if (lane < 8) args.tile_diag[(size_t)slot * 8 + lane] = rec[lane];
         }
     }
     unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
@@ -239,10 +249,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_regen(Sc
         o[0]     = acc.r;
         o[1]     = acc.g;
         o[2]     = acc.b;
-        if (args.tile_diag && lane < 4) {
+        if (args.tile_diag && lane < 8) {
             const uint64_t t_end  = __builtin_amdgcn_s_memrealtime();
-            const uint64_t rec[4] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item };
-            args.tile_diag[(size_t)slot * 4 + lane] = rec[lane];
+            const uint64_t rec[8] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item, 0, 0, 0, 0 };
+            args.tile_diag[(size_t)slot * 8 + lane] = rec[lane];
         }
     }
     unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };

@@ -1783,7 +1783,20 @@ struct Ctx {
     // record k of this lane at deep[k * dstride] (level-major, lanes contiguous)
     float*       deep    = nullptr;
     size_t       dstride = 0;
+#ifdef SP_MEGA_PROF // diagnostic build: shader clocks spent in trace / light sample / eval / occlusion
+    uint64_t prof[4] = { 0, 0, 0, 0 };
+#endif
 };
+#ifdef SP_MEGA_PROF
+#define SP_PROF(k, stmt)                                                                                               \
+    do {                                                                                                               \
+        const uint64_t t_prof_ = __builtin_amdgcn_s_memtime();                                                         \
+        stmt;                                                                                                          \
+        c.prof[k] += __builtin_amdgcn_s_memtime() - t_prof_;                                                           \
+    } while (0)
+#else
+#define SP_PROF(k, stmt) stmt
+#endif
 
 __device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float tmax)
 {
@@ -1816,13 +1829,16 @@ __device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
 {
     rgb L = mkc(0, 0, 0);
     for (int li = 0; li < c.sc.n_lights; ++li) {
-        const Light   l  = uload_light(c.sc.lights + li);
-        const LSample ls = light_sample(c.sc, l, is.p, is.n, next2D(c.rng), c.q);
+        const Light l = uload_light(c.sc.lights + li);
+        LSample     ls;
+        SP_PROF(1, ls = light_sample(c.sc, l, is.p, is.n, next2D(c.rng), c.q));
         if (ls.pdf == 0.0f || cblack(ls.L)) continue;
-        const f3  wi = ls.ray.d;
-        const rgb f  = material_eval(c.sc, is.material, wo, wi, is.n, c.rng, c.q);
-        if (!cblack(f) && !occluded(c, ls.ray, ls.tmin, ls.tmax))
-            L = cadd(L, cdivs(cscale(cmul(f, ls.L), abs_f(dot(wi, is.n))), ls.pdf));
+        const f3 wi = ls.ray.d;
+        rgb      f;
+        SP_PROF(2, f = material_eval(c.sc, is.material, wo, wi, is.n, c.rng, c.q));
+        bool vis = false;
+        if (!cblack(f)) SP_PROF(3, vis = !occluded(c, ls.ray, ls.tmin, ls.tmax));
+        if (vis) L = cadd(L, cdivs(cscale(cmul(f, ls.L), abs_f(dot(wi, is.n))), ls.pdf));
     }
     return L;
 }
@@ -1831,7 +1847,8 @@ __device__ __forceinline__ rgb integrate_direct(Ctx& c, Ray ray)
 {
     rgb L = mkc(0, 0, 0);
     if (0 >= c.sc.max_depth) return L;
-    const Query qr = trace(c, ray, k_ray_epsilon, k_infinite);
+    Query qr;
+    SP_PROF(0, qr = trace(c, ray, k_ray_epsilon, k_infinite));
     if (qr.geom) {
         L = direct_nee(c, qr.is, neg(ray.d));
     } else if (qr.lh.hit) {
