@@ -13,6 +13,7 @@ Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects; see DESIGN
 from __future__ import annotations
 
 import argparse
+import math
 import json
 import os
 import sys
@@ -61,7 +62,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront"])
+    ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront", "chunks"])
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
@@ -193,7 +194,7 @@ def main():
         "config": {"workload": f"{fname} {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
                    "width": args.width, "height": args.height, "spp": args.spp, "integrator": args.integrator,
                    "bvh": "sah" if args.bvh == 0 else "reference", "tiles": int(n_tiles),
-                   "pipeline": ["auto", "megakernel", "wavefront"][stats[-1].pipeline],
+                   "pipeline": ["auto", "megakernel", "wavefront", "chunks"][stats[-1].pipeline],
                    "parallelism": f"tiles{world}"},
         "msamples_per_s": round(msamples, 3),
         "rays_per_step": rays / args.steps,
@@ -236,6 +237,17 @@ def roofline_of(stats, pixels, args, kernel_ms):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    if st.pipeline == 3:  # sample chunks (sp_chunk.hip): four kernels per frame, timed together
+        chunks = max(1, min(16, 1 << max(0, math.ceil(math.log2(max(1.0, 32768 / max(1, (pixels + 63) // 64)))))))
+        snap = chunks * ((pixels + 63) // 64) * 2 * 312 * 64 * 8
+        samples = st.samples
+        # hit record written once, read by the replay and the shade pass; radiance written by the
+        # camera or shade pass and read by the sum; the state snapshots written and read once
+        alg = (st.rng_draws * MT_BYTES_PER_DRAW + samples * (16 * 3 + 12 * 2) + 2 * snap + pixels * PIXEL_BYTES)
+        achieved = alg / (kernel_ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "ck_camera+ck_count+ck_shade+ck_sum",
+                "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg}
     if st.pipeline == 1 or args.integrator != "direct_lighting":  # megakernel, or the sp_wpath rounds
         alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES
         achieved = alg / (kernel_ms * 1e-3) / 1e9

@@ -183,11 +183,13 @@ typedef struct sp_render_params {
     int32_t        flags;             /* SP_PIPELINE_* (0 = automatic)                            */
 } sp_render_params;
 
-/* Device pipeline selection (sp_render_params.flags).  Both produce identical images. */
+/* Device pipeline selection (sp_render_params.flags).  All produce identical images. */
 enum {
-    SP_PIPELINE_AUTO       = 0, /* wavefront where available, else megakernel                   */
+    SP_PIPELINE_AUTO       = 0, /* by work size: wavefront / megakernel / sample chunks (below)   */
     SP_PIPELINE_MEGAKERNEL = 1, /* one lane owns one pixel for all samples (sp_mega.hpp)        */
     SP_PIPELINE_WAVEFRONT  = 2, /* DirectLighting: per-sample primary/shade/shadow kernels       */
+    SP_PIPELINE_SAMPLE_CHUNKS = 3, /* DirectLighting: each pixel's samples in parallel chunks
+                                      (stream state snapshots; sp_chunk.hip)                      */
                                 /* (sp_wave.hip); BruteForceIterative(RR), IterativeRRNEE:      */
                                 /* trace/shade rounds over refilled tile slots (sp_wpath.hip)   */
     SP_RENDER_STAGE_TIMING = 4  /* flag: HIP events between launches fill sp_render_stats.stage_ms */

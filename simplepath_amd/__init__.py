@@ -155,7 +155,7 @@ class ColumnMajorTileScheduler(TileScheduler):
         return shard_tiles(self.get_num_tiles(), rank, world)
 
 
-PIPELINES = {"auto": 0, "megakernel": 1, "wavefront": 2}
+PIPELINES = {"auto": 0, "megakernel": 1, "wavefront": 2, "chunks": 3}
 STAGE_TIMING = 4  # SP_RENDER_STAGE_TIMING
 
 

@@ -1,6 +1,7 @@
 // sp_capi.hip -- extern "C" boundary (include/simplepath_hip.h) and HBM residency of scenes.
 #include "sp_device.hpp"
 #include "sp_wave.hpp"
+#include "sp_chunk.hpp"
 #include "../host/sp_host.hpp"
 
 #include <hip/hip_runtime.h>
@@ -231,6 +232,9 @@ struct sp_scene {
     hipEvent_t           ev_shade[2] = { nullptr, nullptr };
     int                  n_cu         = 0;
     hipEvent_t           ev0 = nullptr, ev1 = nullptr;
+    void*                ck_buf     = nullptr; // sample-chunk pipeline: hits, radiance, snapshots
+    size_t               ck_cap     = 0;
+    int32_t*             ck_ctr     = nullptr;
     float*               d_cost     = nullptr; // megakernel tile order (longest first)
     int32_t*             d_order    = nullptr;
     size_t               order_cap  = 0;
@@ -270,6 +274,9 @@ struct sp_scene {
         if (ev1) (void)hipEventDestroy(ev1);
         if (wp_buf) (void)hipFree(wp_buf);
         if (deep_buf) (void)hipFree(deep_buf);
+        if (ck_buf) (void)hipFree(ck_buf);
+        if (ck_ctr) (void)hipFree(ck_ctr);
+        ck_buf = nullptr; ck_ctr = nullptr; ck_cap = 0;
         if (d_cost) (void)hipFree(d_cost);
         if (d_order) (void)hipFree(d_order);
         d_cost = nullptr; d_order = nullptr; order_cap = 0;
@@ -795,7 +802,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     const bool timing   = (p->flags & SP_RENDER_STAGE_TIMING) != 0;
     float      stage[4] = { 0, 0, 0, 0 };
     int pipeline = p->flags & 3;
-    if (pipeline == 3) return fail(SP_ERR_ARG, "unknown pipeline flag");
+    if (pipeline == SP_PIPELINE_SAMPLE_CHUNKS && integ != SP_INTEGRATOR_DIRECT_LIGHTING)
+        return fail(SP_ERR_UNSUPPORTED, "the sample-chunk pipeline implements DirectLighting");
     const bool wave_ok  = integ == SP_INTEGRATOR_DIRECT_LIGHTING && s->dev.n_lights <= spd::WF_MAX_LIGHTS;
     const bool wpath_ok = spd::wpath_supports(integ);
     if (pipeline == SP_PIPELINE_WAVEFRONT && !wave_ok && !wpath_ok)
@@ -807,12 +815,20 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     // slowest wave, once per sample.  Below SP_WAVE_MIN_TILES tiles (default 24000: between
     // the 1-GPU frame, 32400 tiles, and its 2-GPU shard, 16200) the persistent megakernel,
     // with its tiles taken longest-first, is faster.
-    int64_t wave_min = 24000;
+    // Below SP_CHUNK_MAX_TILES (default 12000: between the 2- and 4-GPU shards) even the
+    // megakernel waits on single pixels' sample chains; the sample-chunk pipeline splits them
+    // (4-GPU shard 1285 -> 1490, 8-GPU shard 823 -> 1384 Mrays/s).
+    int64_t wave_min = 24000, chunk_max = 12000;
     if (const char* v = std::getenv("SP_WAVE_MIN_TILES")) wave_min = std::atoll(v);
-    if (pipeline == SP_PIPELINE_AUTO)
-        pipeline = (wave_ok && n_tiles >= wave_min) ? SP_PIPELINE_WAVEFRONT : SP_PIPELINE_MEGAKERNEL;
+    if (const char* v = std::getenv("SP_CHUNK_MAX_TILES")) chunk_max = std::atoll(v);
+    if (pipeline == SP_PIPELINE_AUTO) {
+        if (wave_ok && n_tiles >= wave_min) pipeline = SP_PIPELINE_WAVEFRONT;
+        else if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && n_tiles < chunk_max) pipeline = SP_PIPELINE_SAMPLE_CHUNKS;
+        else pipeline = SP_PIPELINE_MEGAKERNEL;
+    }
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
-    int launches = 0, parts_used = 1;
+    int                launches = 0, parts_used = 1;
+    unsigned long long ck_camera_rays = 0, ck_samples = 0; // sample-chunk pipeline: counted on the host
     if (pipeline == SP_PIPELINE_WAVEFRONT && wpath_ok) {
         const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
         if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
@@ -971,6 +987,79 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                 }
             }
         }
+    } else if (pipeline == SP_PIPELINE_SAMPLE_CHUNKS) {
+        // sp_chunk.hip: camera rays for all (pixel, sample) at once, a per-pixel replay of the
+        // stream positions with state snapshots at chunk starts, then every (tile, chunk) shaded
+        // in parallel, and the in-order sum.  Chunks per pixel: enough work items to keep the
+        // chip busy when the slowest pixel's chain would otherwise set the frame time.
+        const int    rs_words  = 2 << s->dev.rsqrt_bits;
+        const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
+        if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+        const uint32_t spp    = (uint32_t)p->samples_per_pixel;
+        int64_t        chunks = 1;
+        while (chunks < 16 && n_tiles * chunks < 32768) chunks *= 2;
+        if (const char* v = std::getenv("SP_CHUNKS")) chunks = std::max<int64_t>(1, std::atoll(v));
+        chunks = std::min<int64_t>(chunks, spp);
+        const uint32_t chunk_len = (uint32_t)((spp + chunks - 1) / chunks);
+        chunks                   = (spp + chunk_len - 1) / chunk_len;
+        const size_t n_px     = (size_t)n_tiles * 64;
+        const size_t b_hits   = n_px * spp * 16;
+        const size_t b_L      = n_px * spp * 12;
+        const size_t b_snap   = (size_t)chunks * (size_t)n_tiles * 2 * spm::MT_N * 64 * 8;
+        const size_t b_ctl    = (size_t)chunks * n_px * 4;
+        const size_t need_b   = b_hits + b_L + b_snap + b_ctl + 4 * 256;
+        double       max_gb   = 96.0;
+        if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) max_gb = std::atof(v);
+        if ((double)need_b > max_gb * 1e9)
+            return fail(SP_ERR_UNSUPPORTED, "sample-chunk pipeline: buffers exceed SP_CHUNK_MAX_GB (render fewer tiles per call)");
+        if (need_b > s->ck_cap) {
+            if (s->ck_buf) (void)hipFree(s->ck_buf);
+            s->ck_buf = nullptr;
+            s->ck_cap = 0;
+            SP_HIP(hipMalloc(&s->ck_buf, need_b));
+            s->ck_cap = need_b;
+        }
+        if (!s->ck_ctr) SP_HIP(hipMalloc(&s->ck_ctr, 2 * sizeof(int32_t)));
+        const int    per_cu = spd::chunk_blocks_per_cu(lds_bytes);
+        const int    blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * per_cu, (n_tiles * chunks + 3) / 4));
+        const size_t waves  = (size_t)((n_tiles + 3) / 4) * 4; // ck_count: one wave per tile
+        if (waves > s->mt_waves) {
+            if (s->mt_state) (void)hipFree(s->mt_state);
+            s->mt_state = nullptr;
+            SP_HIP(hipMalloc(&s->mt_state, waves * 2 * spm::MT_N * 64 * sizeof(uint64_t)));
+            s->mt_waves = waves;
+        }
+        char*          base = static_cast<char*>(s->ck_buf);
+        spd::ChunkArgs a{};
+        a.tile_ids  = p->tile_ids ? s->d_tiles : nullptr;
+        a.num_tiles = n_tiles;
+        a.tiles_x   = (s->dev.width + 7) / 8;
+        a.spp       = spp;
+        a.chunks    = (uint32_t)chunks;
+        a.chunk_len = chunk_len;
+        a.n_px      = n_px;
+        a.hits      = reinterpret_cast<float4*>(base);
+        a.L         = reinterpret_cast<float*>(base + b_hits);
+        a.snap      = reinterpret_cast<uint64_t*>(base + b_hits + b_L);
+        a.snap_ctl  = reinterpret_cast<uint32_t*>(base + b_hits + b_L + b_snap);
+        a.mt        = s->mt_state;
+        a.counter   = s->ck_ctr;
+        a.counters  = s->counters;
+        a.out       = d_out;
+        SP_HIP(hipMemsetAsync(s->ck_ctr, 0, 2 * sizeof(int32_t), stream));
+        SP_HIP(hipEventRecord(s->ev0, stream));
+        SP_HIP(spd::chunk_render(s->dev, a, blocks, stream));
+        launches = 4;
+        // camera rays and samples: one per inside pixel and sample (counted here, not on device)
+        int64_t inside = 0;
+        const int32_t tw = (s->dev.width + 7) / 8;
+        for (int64_t sl = 0; sl < n_tiles; ++sl) {
+            const int64_t t  = p->tile_ids ? p->tile_ids[sl] : sl;
+            const int64_t x0 = (t % tw) * 8, y0 = (t / tw) * 8;
+            inside += std::min<int64_t>(8, s->dev.width - x0) * std::min<int64_t>(8, s->dev.height - y0);
+        }
+        ck_camera_rays = s->dev.max_depth > 0 ? (unsigned long long)inside * spp : 0ull;
+        ck_samples     = (unsigned long long)inside * spp;
     } else {
         const int    rs_words  = 2 << s->dev.rsqrt_bits;
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
@@ -1071,6 +1160,10 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         SP_HIP(hipMemcpy(c, s->counters, sizeof(c), hipMemcpyDeviceToHost));
         float ms = 0.0f;
         SP_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        if (pipeline == SP_PIPELINE_SAMPLE_CHUNKS) {
+            c[0] = ck_camera_rays + c[1];
+            c[2] = ck_samples;
+        }
         stats->rays        = c[0];
         stats->shadow_rays = c[1];
         stats->samples     = c[2];

@@ -1,0 +1,275 @@
+// sp_chunk.hip -- DirectLighting with each pixel's samples split into chunks that run in parallel.
+//
+// Why: a pixel's 256 samples draw from one std::mt19937_64 stream (main.cpp:73) in order, and
+// how many words a sample draws depends on what it hit, so the megakernel runs every pixel as one
+// serial chain.  On a 2-8 GPU shard of a 1080p frame the frame then ends with the slowest
+// tile's chain (140 ms of a 141 ms span at 8 GPUs).  This pipeline cuts the chain
+// without changing a single bit of the result:
+//
+//   ck_camera  every (pixel, sample) at once: R2 jitter -> camera ray -> intersect_lights +
+//              intersect (Integrator.cpp:277-283).  Stores the hit record; a light-only hit or a
+//              miss already has its final radiance, stored as the sample's L.
+//   ck_count   per pixel, in sample order: seed the stream, and at every chunk start copy the
+//              generator state (both 312-word buffers + position) to a snapshot.  Between
+//              snapshots it replays only what decides how many words a sample draws:
+//              Light::sample's two draws per light, and the 32 draws of the glossy rho estimate
+//              that Material::eval makes when the sample is valid and wo.y != 0 -- no traversal,
+//              no BSDF arithmetic.
+//   ck_shade   every (tile, chunk) at once: restore the snapshot, then run the reference's
+//              direct_nee for the chunk's samples (same code as the megakernel), store each L.
+//   ck_sum     per pixel: image(p) = (((0 + L_0) + L_1) + ...) / spp, in sample order.
+//
+// Every sample sees the same stream words and the same floating-point sequence as in the
+// megakernel, and the sum runs in the same order, so the image is bit-identical
+// (tests/test_gpu_parity.py).  Camera rays are traced once.  HBM per pixel-sample: 16 B hit
+// record + 12 B radiance written and read back; per (tile, chunk): one 320 KB state snapshot,
+// written by ck_count and used in place (as the working generator state) by ck_shade.
+#include "sp_chunk.hpp"
+#include "sp_mega.hpp"
+
+namespace spd {
+
+namespace {
+
+constexpr uint32_t NO_HIT = 0xffffffffu;
+
+struct Lds {
+    Rsq   q;
+    Stack st;
+};
+
+// shared prologue: rsqrt table + libm tables into LDS, then the wave's traversal stack
+__device__ __forceinline__ Lds lds_setup(const Scene& sc, uint32_t* lds, bool stack)
+{
+    const int tid      = threadIdx.x;
+    const int rs_words = 2 << sc.rsqrt_bits;
+    for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
+    libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
+    __syncthreads();
+    Lds l{ Rsq{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm },
+           Stack{ lds + rs_words + (stack ? (tid >> 6) * sc.stack_words * 64 : 0), tid & 63, sc.stack_depth } };
+    return l;
+}
+
+struct Px {
+    uint32_t x, y;
+    bool     inside;
+};
+__device__ __forceinline__ Px pixel(const Scene& sc, const ChunkArgs& a, int64_t slot, uint32_t lane)
+{
+    const int32_t tile = a.tile_ids ? a.tile_ids[slot] : (int32_t)slot;
+    Px            p;
+    p.x      = (uint32_t)((tile % a.tiles_x) * 8) + morton_decode_1(lane);
+    p.y      = (uint32_t)((tile / a.tiles_x) * 8) + morton_decode_1(lane >> 1);
+    p.inside = (int)p.x < sc.width && (int)p.y < sc.height;
+    return p;
+}
+
+// RSequenceSampler::get_next_2D (math/Sampler.h:158) + PerspectiveCamera::generate_ray_impl
+// (Cameras/Camera.h:119), as in the megakernel's sample loop
+__device__ __forceinline__ Ray camera_ray_px(const Scene& sc, const Px& p, uint32_t i, const Rsq& q)
+{
+    const uint32_t seed2d = ((p.x << 16u) | p.y) ^ 0x6184faf4u;
+    const float    sx     = rseq_component(seed2d, sc.alpha2_0, i);
+    const float    sy     = rseq_component(seed2d, sc.alpha2_1, i);
+    const float    fx     = (float)(int)p.x + sx;
+    const float    fy     = (float)(int)p.y + sy;
+    Ray            ray;
+    ray.o = sc.camera.p;
+    ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
+    return ray;
+}
+
+__device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t v)
+{
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, (unsigned long long)v);
+}
+
+__device__ __forceinline__ int64_t grab(int32_t* counter)
+{
+    int g = 0;
+    if ((threadIdx.x & 63) == 0) g = atomicAdd(counter, 1);
+    return __shfl(g, 0, 64);
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------- camera rays
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_camera(Scene sc, ChunkArgs a)
+{
+    extern __shared__ uint32_t lds[];
+    const Lds      l    = lds_setup(sc, lds, true);
+    const uint32_t lane = threadIdx.x & 63u;
+    const int64_t  item = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (item >= a.num_tiles * (int64_t)a.spp) return;
+    const int64_t  slot = item % a.num_tiles;
+    const uint32_t i    = (uint32_t)(item / a.num_tiles);
+    const Px       px   = pixel(sc, a, slot, lane);
+    const size_t   p    = (size_t)slot * 64 + lane;
+    float4         rec  = make_float4(0.0f, __uint_as_float(NO_HIT), 0.0f, 0.0f);
+    rgb            L    = mkc(0, 0, 0);
+    if (px.inside && sc.max_depth > 0) {
+        // Integrator::integrate's query (Integrator.cpp:277-283), as trace() in sp_path.hpp
+        const Ray      ray = camera_ray_px(sc, px, i, l.q);
+        const LightHit lh  = scene_intersect_lights(sc, ray, k_ray_epsilon, k_infinite, l.st);
+        const Hit      h   = scene_intersect(sc, ray, k_ray_epsilon, lh.hit ? lh.t : k_infinite, l.st);
+        if (h.code != NO_HIT) rec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
+        else if (lh.hit) L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, l.q)));
+    }
+    a.hits[(size_t)i * a.n_px + p]               = rec;
+    a.L[((size_t)i * 3 + 0) * a.n_px + p] = L.r;
+    a.L[((size_t)i * 3 + 1) * a.n_px + p] = L.g;
+    a.L[((size_t)i * 3 + 2) * a.n_px + p] = L.b;
+}
+
+// ------------------------------------------------------------------- stream positions (replay)
+// One wave per tile (the replay is a serial chain per pixel: more waves, shorter frame).
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, ChunkArgs a)
+{
+    extern __shared__ uint32_t lds[];
+    const Lds      l     = lds_setup(sc, lds, false);
+    const uint32_t lane  = threadIdx.x & 63u;
+    const size_t   gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    Rng            rng;
+    rng.base = a.mt + gwave * (2 * MT_N * 64) + lane;
+    while (true) {
+        const int64_t slot = grab(a.counter);
+        if (slot >= a.num_tiles) break;
+        const Px     px = pixel(sc, a, slot, lane);
+        const size_t p  = (size_t)slot * 64 + lane;
+        if (px.inside) rng_seed(rng, ((px.x << 16u) | px.y) ^ 0xb0ae9d99u); // main.cpp:73
+        // hit records do not depend on the stream: load sample i + 1's while sample i is replayed
+        float4 next = px.inside ? a.hits[p] : make_float4(0.0f, __uint_as_float(NO_HIT), 0.0f, 0.0f);
+        for (uint32_t i = 0; i < a.spp; ++i) {
+            const float4 rec = next;
+            if (px.inside && i + 1 < a.spp) next = a.hits[(size_t)(i + 1) * a.n_px + p];
+            if (i % a.chunk_len == 0) {
+                // generator state at the start of chunk i / chunk_len: both buffers + position
+                const size_t   c   = i / a.chunk_len;
+                uint64_t*      dst = a.snap + (c * (size_t)a.num_tiles + (size_t)slot) * (2 * MT_N * 64) + lane;
+                const uint64_t* src = mt_buf(rng, 0);
+                if (px.inside)
+                    for (int k = 0; k < 2 * MT_N; ++k) dst[(size_t)k * 64] = src[(size_t)k * 64];
+                a.snap_ctl[c * a.n_px + p] = (uint32_t)rng.idx | ((uint32_t)rng.cur << 16) | ((uint32_t)rng.ready << 17);
+            }
+            if (!px.inside) continue;
+            rng_prepare(rng);
+            const uint32_t code = __float_as_uint(rec.y);
+            if (code == NO_HIT) continue;
+            // direct_nee (sp_path.hpp): per light, 2 draws for Light::sample; if the sample is
+            // usable, Material::eval draws 32 words for a glossy base (16 two-word Beckmann
+            // samples of the rho estimate) unless wo.y == 0 in the shading frame, else none
+            const Ray   ray = camera_ray_px(sc, px, i, l.q);
+            const Hit   h{ rec.x, code, rec.z, rec.w };
+            const Isect is  = finish_hit(sc, h, ray, l.q);
+            const f3    wo  = neg(ray.d);
+            for (int li = 0; li < sc.n_lights; ++li) {
+                const Light   lt = uload_light(sc.lights + li);
+                const LSample ls = light_sample(sc, lt, is.p, is.n, next2D(rng), l.q);
+                if (ls.pdf == 0.0f || cblack(ls.L)) continue;
+                const Material& m    = sc.materials[is.material];
+                const int       base = (m.kind == SP_MAT_CLEARCOAT) ? sc.materials[m.base].kind : m.kind;
+                if (base == SP_MAT_LAMBERTIAN) continue;
+                const Onb o = onb_from_v(is.n, l.q);
+                if (to_onb(o, wo).y != 0.0f) rng_skip(rng, 32);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------- chunked shading
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_shade(Scene sc, ChunkArgs a)
+{
+    extern __shared__ uint32_t lds[];
+    const Lds      l     = lds_setup(sc, lds, true);
+    const uint32_t lane  = threadIdx.x & 63u;
+    Rng            rng;
+    uint64_t       shadow_total = 0, draws_total = 0;
+    while (true) {
+        const int64_t item = grab(a.counter + 1);
+        if (item >= a.num_tiles * (int64_t)a.chunks) break;
+        // a tile's chunks are adjacent in the queue, so a slow tile's chunks run side by side
+        const int64_t  slot = item / a.chunks;
+        const uint32_t c    = (uint32_t)(item % a.chunks);
+        const Px       px   = pixel(sc, a, slot, lane);
+        const size_t   p    = (size_t)slot * 64 + lane;
+        const uint32_t i0   = c * a.chunk_len;
+        const uint32_t i1   = min(a.spp, i0 + a.chunk_len);
+        if (px.inside && i0 < i1) {
+        // the snapshot has the working state's layout: the generator runs in place (each
+        // snapshot is used by exactly this item)
+        rng.base = a.snap + ((size_t)c * (size_t)a.num_tiles + (size_t)slot) * (2 * MT_N * 64) + lane;
+        const uint32_t st = a.snap_ctl[(size_t)c * a.n_px + p];
+        rng.idx   = (int)(st & 0xffffu);
+        rng.cur   = (int)((st >> 16) & 1u);
+        rng.ready = (int)((st >> 17) & 1u);
+        rng.draws = 0;
+        rng.pfn   = 0;
+        Ctx ctx{ sc, rng, l.q, l.st, 0u, 0u };
+        for (uint32_t i = i0; i < i1; ++i) {
+            rng_prepare(rng);
+            const float4   rec  = a.hits[(size_t)i * a.n_px + p];
+            const uint32_t code = __float_as_uint(rec.y);
+            if (code == NO_HIT) continue; // miss or light-only hit: L was stored by ck_camera
+            const Ray   ray = camera_ray_px(sc, px, i, l.q);
+            const Hit   h{ rec.x, code, rec.z, rec.w };
+            const Isect is  = finish_hit(sc, h, ray, l.q);
+            const rgb   L   = direct_nee(ctx, is, neg(ray.d));
+            a.L[((size_t)i * 3 + 0) * a.n_px + p] = L.r;
+            a.L[((size_t)i * 3 + 1) * a.n_px + p] = L.g;
+            a.L[((size_t)i * 3 + 2) * a.n_px + p] = L.b;
+        }
+        shadow_total += ctx.shadow;
+        draws_total += rng.draws;
+        }
+    }
+    wave_add(a.counters + 1, shadow_total);
+    wave_add(a.counters + 3, draws_total);
+}
+
+// ------------------------------------------------------------------------------ resolve
+__global__ void __launch_bounds__(256) ck_sum(Scene sc, ChunkArgs a)
+{
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= (int64_t)a.n_px) return;
+    const Px px  = pixel(sc, a, p >> 6, (uint32_t)p & 63u);
+    rgb      acc = mkc(0, 0, 0);
+    if (px.inside) {
+        for (uint32_t i = 0; i < a.spp; ++i)
+            acc = cadd(acc, mkc(a.L[((size_t)i * 3 + 0) * a.n_px + p], a.L[((size_t)i * 3 + 1) * a.n_px + p],
+                                a.L[((size_t)i * 3 + 2) * a.n_px + p])); // image(p) += integrate(...)
+        acc = cdivs(acc, (float)a.spp);                                    // image(p) /= num_pixel_samples
+    }
+    a.out[(size_t)p * 3 + 0] = acc.r;
+    a.out[(size_t)p * 3 + 1] = acc.g;
+    a.out[(size_t)p * 3 + 2] = acc.b;
+}
+
+int chunk_blocks_per_cu(size_t lds_bytes)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ck_shade, 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess) return 1;
+    return n > 0 ? n : 1;
+}
+
+hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, hipStream_t stream)
+{
+    const size_t rs_bytes    = (size_t)(2 << sc.rsqrt_bits) * 4;
+    const size_t stack_bytes = (size_t)WAVES_PER_BLOCK * sc.stack_words * 64 * 4;
+    const int64_t cam_waves  = a.num_tiles * (int64_t)a.spp;
+    hipLaunchKernelGGL(ck_camera, dim3((unsigned)((cam_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
+                       dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes, stream, sc, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ck_count, dim3((unsigned)((a.num_tiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
+                       dim3(64 * WAVES_PER_BLOCK), rs_bytes, stream, sc, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(ck_shade, dim3((unsigned)persistent_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes, stream,
+                       sc, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(ck_sum, dim3((unsigned)((a.n_px + 255) / 256)), dim3(256), 0, stream, sc, a);
+    return hipGetLastError();
+}
+
+} // namespace spd

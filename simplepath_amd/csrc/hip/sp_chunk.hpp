@@ -1,0 +1,28 @@
+// sp_chunk.hpp -- sample-chunked DirectLighting (sp_chunk.hip): host-visible launch interface.
+#pragma once
+#include "sp_device.hpp"
+
+namespace spd {
+
+struct ChunkArgs {
+    const int32_t*      tile_ids;  // caller's tile list (nullptr: slot = tile)
+    int64_t             num_tiles;
+    int32_t             tiles_x;
+    uint32_t            spp;
+    uint32_t            chunks;    // sample chunks per pixel
+    uint32_t            chunk_len; // samples per chunk (ceil(spp / chunks))
+    size_t              n_px;      // num_tiles * 64 pixel slots
+    float4*             hits;      // [spp][n_px] {t, code, beta, gamma}; code 0xffffffff = no geometry
+    float*              L;         // [spp][3][n_px] per-sample radiance
+    uint64_t*           snap;      // [chunks][num_tiles][2 * 312][64] generator buffers
+    uint32_t*           snap_ctl;  // [chunks][n_px] idx | cur << 16 | ready << 17
+    uint64_t*           mt;        // ck_count, one wave per tile: [num_tiles][2][312][64] working state
+    int32_t*            counter;   // [2] work queues of ck_count and ck_shade (zeroed by the caller)
+    unsigned long long* counters;  // stats: [1] shadow rays, [3] RNG draws
+    float*              out;       // tile-packed radiance [n_px][3]
+};
+
+int        chunk_blocks_per_cu(size_t lds_bytes);
+hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, hipStream_t stream);
+
+} // namespace spd

@@ -139,6 +139,25 @@ __device__ __forceinline__ uint64_t rng_raw(Rng& r)
     return mt_temper(w);
 }
 
+// Advance the stream by n draws without reading them: the same state (buffers, position,
+// twists) as n rng_raw calls.  Used where only the count of a span of draws is known.
+__device__ __forceinline__ void rng_skip(Rng& r, int n)
+{
+    while (n > 0) {
+        if (r.idx >= MT_N) {
+            if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
+            r.cur ^= 1;
+            r.idx   = 0;
+            r.ready = 0;
+        }
+        const int take = (n < MT_N - r.idx) ? n : MT_N - r.idx;
+        r.idx += take;
+        r.draws += (uint32_t)take;
+        n -= take;
+    }
+    r.pfn = 0;
+}
+
 // IncoherentSampler::get_next_1D / get_next_2D (math/Sampler.h:110-118)
 __device__ __forceinline__ float next1D(Rng& r) { return canonical_from_u64(rng_raw(r)); }
 struct P2 {

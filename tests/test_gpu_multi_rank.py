@@ -2,8 +2,8 @@
 collective runs over gloo on host copies; on a node each rank owns a GPU and bench.py gathers
 over RCCL with the same shard.gather_frame), each renders its interleaved shard with the HIP
 path, and the frame assembled on rank 0 must equal one process rendering every tile, bit for
-bit.  Shards this small run on the persistent megakernel (AUTO below 24000 tiles), the full
-frame on the wavefront, so this also checks that the two agree through the multi-rank path."""
+bit.  Shards this small run on the sample-chunk pipeline (AUTO below 12000 tiles), the full
+frame here on the wavefront, so this also checks that the two agree through the multi-rank path."""
 import os
 import socket
 
@@ -40,7 +40,7 @@ def _worker(rank, world, port, scene_path, w, h, spp, result_path):
     n = sp.TileScheduler(w, h).get_num_tiles()
     mine = shard.shard_tiles(n, rank, world)
     tiles, st = sp.render_tiles(scene, "direct_lighting", spp, mine)
-    assert st.pipeline == 1  # megakernel for a shard this small
+    assert st.pipeline == 3  # AUTO: sample chunks for a shard this small
     local = torch.zeros((shard.per_rank_capacity(n, world), 64, 3), dtype=torch.float32)
     local[: len(mine)] = torch.from_numpy(tiles)
     frame = shard.gather_frame(local, n, rank, world, dist)

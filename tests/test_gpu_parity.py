@@ -30,7 +30,7 @@ def load(scene_dir, name, w, h, bvh):
     return s
 
 
-@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront", "chunks"])
 def test_bunny_direct_lighting_bitexact(scene_dir, pipeline):
     s = load(scene_dir, "bunny.sp", 64, 40, bvh=1)
     g, gst = sp.render_tiles(s, "direct_lighting", 4, pipeline=pipeline)
@@ -129,6 +129,34 @@ def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
     assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
         (wst.rays, wst.shadow_rays, wst.samples, wst.rng_draws)
     assert wst.launches == 3 + 4 * 5 and mst.launches == 1
+
+
+@pytest.mark.parametrize("scene,bvh,chunks", [("bunny.sp", 0, "0"), ("bunny.sp", 1, "3"), ("material_spheres_ibl.sp", 0, "7"),
+                                              ("material_spheres.sp", 1, "16")])
+def test_sample_chunks_equal_megakernel(scene_dir, monkeypatch, scene, bvh, chunks):
+    # each pixel's samples split into chunks that start from replayed generator snapshots: every
+    # sample sees the same stream words, the sum keeps sample order -> bit-identical image and
+    # identical ray / draw counts.  Chunk counts that do not divide spp (13) leave a short last
+    # chunk; "0" = automatic (16 for this many tiles).
+    if chunks != "0":
+        monkeypatch.setenv("SP_CHUNKS", chunks)
+    s = load(scene_dir, scene, 72, 40, bvh=bvh)
+    m, mst = sp.render_tiles(s, "direct_lighting", 13, pipeline="megakernel")
+    c, cst = sp.render_tiles(s, "direct_lighting", 13, pipeline="chunks")
+    assert cst.pipeline == 3 and cst.launches == 4
+    assert np.array_equal(m.view(np.uint32), c.view(np.uint32)), rel_l2(c, m)
+    assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
+        (cst.rays, cst.shadow_rays, cst.samples, cst.rng_draws)
+
+
+def test_sample_chunks_tile_subset_matches_oracle(scene_dir):
+    # a ragged tile subset (a rank's shard) through the chunk pipeline vs the CPU oracle
+    s = load(scene_dir, "bunny.sp", 100, 60, bvh=1)
+    tiles = np.arange(1, sp.TileScheduler(100, 60).get_num_tiles(), 2, dtype=np.int32)
+    g, gst = sp.render_tiles(s, "direct_lighting", 6, tiles, pipeline="chunks")
+    c, cst = _oracle.render(s, sp.string_to_integrator_type("direct_lighting"), 6, tiles, variant="spm")
+    assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
 
 
 def test_wavefront_two_parts(scene_dir, monkeypatch):
