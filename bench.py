@@ -238,7 +238,9 @@ def roofline_of(stats, pixels, args, kernel_ms):
         except Exception:
             traffic = None
     if st.pipeline == 3:  # sample chunks (sp_chunk.hip): four kernels per frame, timed together
-        chunks = max(1, min(16, 1 << max(0, math.ceil(math.log2(max(1.0, 32768 / max(1, (pixels + 63) // 64)))))))
+        tiles, chunks = (pixels + 63) // 64, 1
+        while chunks < 16 and tiles * chunks < 16384:  # sp_capi.hip's choice
+            chunks *= 2
         snap = chunks * ((pixels + 63) // 64) * 2 * 312 * 64 * 8
         samples = st.samples
         # hit record written once, read by the replay and the shade pass; radiance written by the

@@ -997,7 +997,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         const uint32_t spp    = (uint32_t)p->samples_per_pixel;
         int64_t        chunks = 1;
-        while (chunks < 16 && n_tiles * chunks < 32768) chunks *= 2;
+        while (chunks < 16 && n_tiles * chunks < 16384) chunks *= 2;
         if (const char* v = std::getenv("SP_CHUNKS")) chunks = std::max<int64_t>(1, std::atoll(v));
         chunks = std::min<int64_t>(chunks, spp);
         const uint32_t chunk_len = (uint32_t)((spp + chunks - 1) / chunks);
@@ -1007,7 +1007,14 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         const size_t b_L      = n_px * spp * 12;
         const size_t b_snap   = (size_t)chunks * (size_t)n_tiles * 2 * spm::MT_N * 64 * 8;
         const size_t b_ctl    = (size_t)chunks * n_px * 4;
-        const size_t need_b   = b_hits + b_L + b_snap + b_ctl + 4 * 256;
+        // per-sample draw counts from the camera pass unless an image light makes them depend on
+        // the drawn numbers (then ck_count replays Light::sample)
+        bool known_draws = s->dev.n_lights <= 1000;
+        for (const auto& l : s->host->lights)
+            if (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) known_draws = false;
+        if (const char* v = std::getenv("SP_CHUNK_REPLAY")) known_draws = known_draws && std::atoi(v) == 0;
+        const size_t b_draws  = known_draws ? n_px * spp * 2 : 0;
+        const size_t need_b   = b_hits + b_L + b_snap + b_ctl + b_draws + 4 * 256;
         double       max_gb   = 96.0;
         if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) max_gb = std::atof(v);
         if ((double)need_b > max_gb * 1e9)
@@ -1042,6 +1049,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         a.L         = reinterpret_cast<float*>(base + b_hits);
         a.snap      = reinterpret_cast<uint64_t*>(base + b_hits + b_L);
         a.snap_ctl  = reinterpret_cast<uint32_t*>(base + b_hits + b_L + b_snap);
+        a.draws     = known_draws ? reinterpret_cast<uint16_t*>(base + b_hits + b_L + b_snap + b_ctl) : nullptr;
         a.mt        = s->mt_state;
         a.counter   = s->ck_ctr;
         a.counters  = s->counters;

@@ -93,6 +93,30 @@ __device__ __forceinline__ int64_t grab(int32_t* counter)
     return __shfl(g, 0, 64);
 }
 
+// Stream words one DirectLighting sample at hit `is` draws (direct_nee, sp_path.hpp): two per
+// light for Light::sample, plus 32 for the glossy rho estimate of Material::eval when the light
+// sample is usable and wo.y != 0 in the shading frame.  For sphere and uniform environment
+// lights usability (pdf != 0, L not black) does not depend on the drawn numbers -- pdf is
+// sphere_pdf(observer) or a constant, L the radiance -- so the count is known from the hit.
+__device__ __forceinline__ uint32_t sample_draws(const Scene& sc, const Isect& is, f3 wo, const Rsq& q)
+{
+    const Material& m    = sc.materials[is.material];
+    const int       base = (m.kind == SP_MAT_CLEARCOAT) ? sc.materials[m.base].kind : m.kind;
+    bool            rho  = false;
+    if (base != SP_MAT_LAMBERTIAN) {
+        const Onb o = onb_from_v(is.n, q);
+        rho         = to_onb(o, wo).y != 0.0f;
+    }
+    uint32_t n = 0;
+    for (int li = 0; li < sc.n_lights; ++li) {
+        const Light lt  = uload_light(sc.lights + li);
+        const float pdf = (lt.kind == SP_LIGHT_SPHERE) ? sphere_pdf(lt, is.p) : k_uniform_sphere_pdf;
+        n += 2;
+        if (rho && !(pdf == 0.0f || cblack(lt.radiance))) n += 32;
+    }
+    return n;
+}
+
 } // namespace
 
 // ---------------------------------------------------------------------------- camera rays
@@ -109,14 +133,20 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_camera(Scene sc, Chun
     const size_t   p    = (size_t)slot * 64 + lane;
     float4         rec  = make_float4(0.0f, __uint_as_float(NO_HIT), 0.0f, 0.0f);
     rgb            L    = mkc(0, 0, 0);
+    uint32_t       ndraw = 0;
     if (px.inside && sc.max_depth > 0) {
         // Integrator::integrate's query (Integrator.cpp:277-283), as trace() in sp_path.hpp
         const Ray      ray = camera_ray_px(sc, px, i, l.q);
         const LightHit lh  = scene_intersect_lights(sc, ray, k_ray_epsilon, k_infinite, l.st);
         const Hit      h   = scene_intersect(sc, ray, k_ray_epsilon, lh.hit ? lh.t : k_infinite, l.st);
-        if (h.code != NO_HIT) rec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
-        else if (lh.hit) L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, l.q)));
+        if (h.code != NO_HIT) {
+            rec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
+            if (a.draws) ndraw = sample_draws(sc, finish_hit(sc, h, ray, l.q), neg(ray.d), l.q);
+        } else if (lh.hit) {
+            L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, l.q)));
+        }
     }
+    if (a.draws) a.draws[(size_t)i * a.n_px + p] = (uint16_t)ndraw;
     a.hits[(size_t)i * a.n_px + p]               = rec;
     a.L[((size_t)i * 3 + 0) * a.n_px + p] = L.r;
     a.L[((size_t)i * 3 + 1) * a.n_px + p] = L.g;
@@ -149,11 +179,19 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
                 const size_t   c   = i / a.chunk_len;
                 uint64_t*      dst = a.snap + (c * (size_t)a.num_tiles + (size_t)slot) * (2 * MT_N * 64) + lane;
                 const uint64_t* src = mt_buf(rng, 0);
-                if (px.inside)
-                    for (int k = 0; k < 2 * MT_N; ++k) dst[(size_t)k * 64] = src[(size_t)k * 64];
+                // the buffer being consumed; the other one only if it already holds the next
+                // generation (ready), else it is scratch that the first wrap overwrites
+                if (px.inside) {
+                    const int k0 = rng.ready ? 0 : rng.cur * MT_N, k1 = rng.ready ? 2 * MT_N : k0 + MT_N;
+                    for (int k = k0; k < k1; ++k) dst[(size_t)k * 64] = src[(size_t)k * 64];
+                }
                 a.snap_ctl[c * a.n_px + p] = (uint32_t)rng.idx | ((uint32_t)rng.cur << 16) | ((uint32_t)rng.ready << 17);
             }
             if (!px.inside) continue;
+            if (a.draws) { // counts known from the camera pass: advance the stream only
+                rng_skip(rng, a.draws[(size_t)i * a.n_px + p]);
+                continue;
+            }
             rng_prepare(rng);
             const uint32_t code = __float_as_uint(rec.y);
             if (code == NO_HIT) continue;

@@ -14,6 +14,8 @@ struct ChunkArgs {
     size_t              n_px;      // num_tiles * 64 pixel slots
     float4*             hits;      // [spp][n_px] {t, code, beta, gamma}; code 0xffffffff = no geometry
     float*              L;         // [spp][3][n_px] per-sample radiance
+    uint16_t*           draws;     // [spp][n_px] stream words each sample draws, when the camera pass
+                                   // can tell (no image light); nullptr: ck_count replays Light::sample
     uint64_t*           snap;      // [chunks][num_tiles][2 * 312][64] generator buffers
     uint32_t*           snap_ctl;  // [chunks][n_px] idx | cur << 16 | ready << 17
     uint64_t*           mt;        // ck_count, one wave per tile: [num_tiles][2][312][64] working state

@@ -131,15 +131,18 @@ def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
     assert wst.launches == 3 + 4 * 5 and mst.launches == 1
 
 
-@pytest.mark.parametrize("scene,bvh,chunks", [("bunny.sp", 0, "0"), ("bunny.sp", 1, "3"), ("material_spheres_ibl.sp", 0, "7"),
-                                              ("material_spheres.sp", 1, "16")])
-def test_sample_chunks_equal_megakernel(scene_dir, monkeypatch, scene, bvh, chunks):
-    # each pixel's samples split into chunks that start from replayed generator snapshots: every
-    # sample sees the same stream words, the sum keeps sample order -> bit-identical image and
-    # identical ray / draw counts.  Chunk counts that do not divide spp (13) leave a short last
-    # chunk; "0" = automatic (16 for this many tiles).
+@pytest.mark.parametrize("scene,bvh,chunks,replay", [("bunny.sp", 0, "0", "0"), ("bunny.sp", 1, "3", "0"),
+                                                     ("bunny.sp", 0, "5", "1"), ("material_spheres_ibl.sp", 0, "7", "0"),
+                                                     ("material_spheres.sp", 1, "16", "0"), ("closed_room.sp", 0, "4", "0")])
+def test_sample_chunks_equal_megakernel(scene_dir, monkeypatch, scene, bvh, chunks, replay):
+    # each pixel's samples split into chunks that start from generator snapshots: every sample
+    # sees the same stream words, the sum keeps sample order -> bit-identical image and identical
+    # ray / draw counts.  Chunk counts that do not divide spp (13) leave a short last chunk; "0" =
+    # automatic (16 for this many tiles).  Draw counts come from the camera pass, or from the
+    # Light::sample replay (image light, or SP_CHUNK_REPLAY=1).
     if chunks != "0":
         monkeypatch.setenv("SP_CHUNKS", chunks)
+    monkeypatch.setenv("SP_CHUNK_REPLAY", replay)
     s = load(scene_dir, scene, 72, 40, bvh=bvh)
     m, mst = sp.render_tiles(s, "direct_lighting", 13, pipeline="megakernel")
     c, cst = sp.render_tiles(s, "direct_lighting", 13, pipeline="chunks")
