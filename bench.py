@@ -238,14 +238,10 @@ def roofline_of(stats, pixels, args, kernel_ms):
         except Exception:
             traffic = None
     if st.pipeline == 3:  # sample chunks (sp_chunk.hip): four kernels per frame, timed together
-        tiles, chunks = (pixels + 63) // 64, 1
-        while chunks < 16 and tiles * chunks < 16384:  # sp_capi.hip's choice
-            chunks *= 2
-        snap = chunks * ((pixels + 63) // 64) * 2 * 312 * 64 * 8
         samples = st.samples
-        # hit record written once, read by the replay and the shade pass; radiance written by the
-        # camera or shade pass and read by the sum; the state snapshots written and read once
-        alg = (st.rng_draws * MT_BYTES_PER_DRAW + samples * (16 * 3 + 12 * 2) + 2 * snap + pixels * PIXEL_BYTES)
+        # draws at 24 B (read + the twist of its generation), the hit record written once and read
+        # by ck_count and ck_shade, the 2-byte draw count, radiance written once and summed
+        alg = st.rng_draws * MT_BYTES_PER_DRAW + samples * (16 * 3 + 2 * 2 + 12 * 2) + pixels * PIXEL_BYTES
         achieved = alg / (kernel_ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "ck_camera+ck_count+ck_shade+ck_sum",

@@ -1005,7 +1005,12 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         const size_t n_px     = (size_t)n_tiles * 64;
         const size_t b_hits   = n_px * spp * 16;
         const size_t b_L      = n_px * spp * 12;
-        const size_t b_snap   = (size_t)chunks * (size_t)n_tiles * 2 * spm::MT_N * 64 * 8;
+        // generator store: every generation a pixel's stream reaches; a DirectLighting sample draws
+        // at most 34 words per light (Light::sample 2 + glossy rho estimate 32), +2 generations for
+        // the first twist and the one rng_prepare may twist ahead
+        const uint64_t max_draws = (uint64_t)spp * (uint64_t)std::max(1, s->dev.n_lights) * 34;
+        const uint32_t gens      = (uint32_t)((max_draws + spm::MT_N - 1) / spm::MT_N + 2);
+        const size_t b_snap   = (size_t)n_tiles * gens * spm::MT_N * 64 * 8;
         const size_t b_ctl    = (size_t)chunks * n_px * 4;
         // per-sample draw counts from the camera pass unless an image light makes them depend on
         // the drawn numbers (then ck_count replays Light::sample)
@@ -1029,13 +1034,6 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         if (!s->ck_ctr) SP_HIP(hipMalloc(&s->ck_ctr, 2 * sizeof(int32_t)));
         const int    per_cu = spd::chunk_blocks_per_cu(lds_bytes);
         const int    blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * per_cu, (n_tiles * chunks + 3) / 4));
-        const size_t waves  = (size_t)((n_tiles + 3) / 4) * 4; // ck_count: one wave per tile
-        if (waves > s->mt_waves) {
-            if (s->mt_state) (void)hipFree(s->mt_state);
-            s->mt_state = nullptr;
-            SP_HIP(hipMalloc(&s->mt_state, waves * 2 * spm::MT_N * 64 * sizeof(uint64_t)));
-            s->mt_waves = waves;
-        }
         char*          base = static_cast<char*>(s->ck_buf);
         spd::ChunkArgs a{};
         a.tile_ids  = p->tile_ids ? s->d_tiles : nullptr;
@@ -1047,10 +1045,10 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         a.n_px      = n_px;
         a.hits      = reinterpret_cast<float4*>(base);
         a.L         = reinterpret_cast<float*>(base + b_hits);
-        a.snap      = reinterpret_cast<uint64_t*>(base + b_hits + b_L);
+        a.gens        = reinterpret_cast<uint64_t*>(base + b_hits + b_L);
+        a.gens_per_px = gens;
         a.snap_ctl  = reinterpret_cast<uint32_t*>(base + b_hits + b_L + b_snap);
         a.draws     = known_draws ? reinterpret_cast<uint16_t*>(base + b_hits + b_L + b_snap + b_ctl) : nullptr;
-        a.mt        = s->mt_state;
         a.counter   = s->ck_ctr;
         a.counters  = s->counters;
         a.out       = d_out;

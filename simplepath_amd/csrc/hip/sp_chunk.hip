@@ -9,21 +9,20 @@
 //   ck_camera  every (pixel, sample) at once: R2 jitter -> camera ray -> intersect_lights +
 //              intersect (Integrator.cpp:277-283).  Stores the hit record; a light-only hit or a
 //              miss already has its final radiance, stored as the sample's L.
-//   ck_count   per pixel, in sample order: seed the stream, and at every chunk start copy the
-//              generator state (both 312-word buffers + position) to a snapshot.  Between
-//              snapshots it replays only what decides how many words a sample draws:
-//              Light::sample's two draws per light, and the 32 draws of the glossy rho estimate
-//              that Material::eval makes when the sample is valid and wo.y != 0 -- no traversal,
-//              no BSDF arithmetic.
-//   ck_shade   every (tile, chunk) at once: restore the snapshot, then run the reference's
-//              direct_nee for the chunk's samples (same code as the megakernel), store each L.
+//   ck_count   per pixel, in sample order: seed the stream and advance it by each sample's draw
+//              count (from ck_camera; with an image light, by replaying Light::sample, whose
+//              usability then depends on the drawn numbers), writing every generation of the
+//              stream into the pixel's store and the position at every chunk start.
+//   ck_shade   every (tile, chunk) at once: start at the chunk's position in the store (no
+//              twisting: the generations are there), run the reference's direct_nee for the
+//              chunk's samples (same code as the megakernel), store each L.
 //   ck_sum     per pixel: image(p) = (((0 + L_0) + L_1) + ...) / spp, in sample order.
 //
 // Every sample sees the same stream words and the same floating-point sequence as in the
 // megakernel, and the sum runs in the same order, so the image is bit-identical
-// (tests/test_gpu_parity.py).  Camera rays are traced once.  HBM per pixel-sample: 16 B hit
-// record + 12 B radiance written and read back; per (tile, chunk): one 320 KB state snapshot,
-// written by ck_count and used in place (as the working generator state) by ck_shade.
+// (tests/test_gpu_parity.py).  Camera rays are traced once, and each generation of a stream is
+// twisted once.  HBM per pixel-sample: 16 B hit record + 2 B draw count + 12 B radiance written
+// and read back; per pixel: 2.5 KB per 312 draws of generator store.
 #include "sp_chunk.hpp"
 #include "sp_mega.hpp"
 
@@ -160,33 +159,22 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
     extern __shared__ uint32_t lds[];
     const Lds      l     = lds_setup(sc, lds, false);
     const uint32_t lane  = threadIdx.x & 63u;
-    const size_t   gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
     Rng            rng;
-    rng.base = a.mt + gwave * (2 * MT_N * 64) + lane;
+    rng.lin = 1; // successive generations side by side in the pixel's store
     while (true) {
         const int64_t slot = grab(a.counter);
         if (slot >= a.num_tiles) break;
         const Px     px = pixel(sc, a, slot, lane);
         const size_t p  = (size_t)slot * 64 + lane;
+        rng.base        = a.gens + (size_t)slot * a.gens_per_px * (MT_N * 64) + lane;
         if (px.inside) rng_seed(rng, ((px.x << 16u) | px.y) ^ 0xb0ae9d99u); // main.cpp:73
         // hit records do not depend on the stream: load sample i + 1's while sample i is replayed
         float4 next = px.inside ? a.hits[p] : make_float4(0.0f, __uint_as_float(NO_HIT), 0.0f, 0.0f);
         for (uint32_t i = 0; i < a.spp; ++i) {
             const float4 rec = next;
             if (px.inside && i + 1 < a.spp) next = a.hits[(size_t)(i + 1) * a.n_px + p];
-            if (i % a.chunk_len == 0) {
-                // generator state at the start of chunk i / chunk_len: both buffers + position
-                const size_t   c   = i / a.chunk_len;
-                uint64_t*      dst = a.snap + (c * (size_t)a.num_tiles + (size_t)slot) * (2 * MT_N * 64) + lane;
-                const uint64_t* src = mt_buf(rng, 0);
-                // the buffer being consumed; the other one only if it already holds the next
-                // generation (ready), else it is scratch that the first wrap overwrites
-                if (px.inside) {
-                    const int k0 = rng.ready ? 0 : rng.cur * MT_N, k1 = rng.ready ? 2 * MT_N : k0 + MT_N;
-                    for (int k = k0; k < k1; ++k) dst[(size_t)k * 64] = src[(size_t)k * 64];
-                }
-                a.snap_ctl[c * a.n_px + p] = (uint32_t)rng.idx | ((uint32_t)rng.cur << 16) | ((uint32_t)rng.ready << 17);
-            }
+            if (i % a.chunk_len == 0) // stream position at the start of chunk i / chunk_len
+                a.snap_ctl[(size_t)(i / a.chunk_len) * a.n_px + p] = (uint32_t)rng.idx | ((uint32_t)rng.cur << 16);
             if (!px.inside) continue;
             if (a.draws) { // counts known from the camera pass: advance the stream only
                 rng_skip(rng, a.draws[(size_t)i * a.n_px + p]);
@@ -235,13 +223,14 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_shade(Scene sc, Chunk
         const uint32_t i0   = c * a.chunk_len;
         const uint32_t i1   = min(a.spp, i0 + a.chunk_len);
         if (px.inside && i0 < i1) {
-        // the snapshot has the working state's layout: the generator runs in place (each
-        // snapshot is used by exactly this item)
-        rng.base = a.snap + ((size_t)c * (size_t)a.num_tiles + (size_t)slot) * (2 * MT_N * 64) + lane;
+        // every generation this chunk draws from was written by ck_count: read-only stream
         const uint32_t st = a.snap_ctl[(size_t)c * a.n_px + p];
+        rng.base  = a.gens + (size_t)slot * a.gens_per_px * (MT_N * 64) + lane;
         rng.idx   = (int)(st & 0xffffu);
-        rng.cur   = (int)((st >> 16) & 1u);
-        rng.ready = (int)((st >> 17) & 1u);
+        rng.cur   = (int)(st >> 16);
+        rng.lin   = 1;
+        rng.pre   = 1;
+        rng.ready = 1;
         rng.draws = 0;
         rng.pfn   = 0;
         Ctx ctx{ sc, rng, l.q, l.st, 0u, 0u };

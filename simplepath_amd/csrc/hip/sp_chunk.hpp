@@ -16,9 +16,10 @@ struct ChunkArgs {
     float*              L;         // [spp][3][n_px] per-sample radiance
     uint16_t*           draws;     // [spp][n_px] stream words each sample draws, when the camera pass
                                    // can tell (no image light); nullptr: ck_count replays Light::sample
-    uint64_t*           snap;      // [chunks][num_tiles][2 * 312][64] generator buffers
-    uint32_t*           snap_ctl;  // [chunks][n_px] idx | cur << 16 | ready << 17
-    uint64_t*           mt;        // ck_count, one wave per tile: [num_tiles][2][312][64] working state
+    uint64_t*           gens;      // [num_tiles][gens_per_px][312][64]: every generation of each pixel's
+                                   // mt19937_64 stream, written once by ck_count, read by ck_shade
+    uint32_t            gens_per_px;
+    uint32_t*           snap_ctl;  // [chunks][n_px] stream position at each chunk start: idx | gen << 16
     int32_t*            counter;   // [2] work queues of ck_count and ck_shade (zeroed by the caller)
     unsigned long long* counters;  // stats: [1] shadow rays, [3] RNG draws
     float*              out;       // tile-packed radiance [n_px][3]

@@ -47,11 +47,16 @@ struct Rng {
     int       idx;   // next word in it
     int       ready; // other buffer already holds the next generation
     uint32_t  draws;
+    // Generation store (sp_chunk.hip): with lin, buffer b + 1 follows buffer b (a per-pixel array
+    // of successive generations) instead of the two-buffer ring; with pre, every generation is
+    // already there, so a buffer switch never twists.
+    int       lin = 0, pre = 0;
     int       pfn = 0;        // valid words in pf (words idx .. idx + pfn - 1 of buffer cur)
     uint64_t  pf[RNG_PF > 0 ? RNG_PF : 1];
 };
 
 __device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_N * 64; }
+__device__ __forceinline__ int       mt_next(const Rng& r) { return r.lin ? r.cur + 1 : r.cur ^ 1; }
 
 // B = twist(A) without modifying A (in-place MT19937-64 twist split over two buffers).
 __device__ __forceinline__ void mt_twist_into(const uint64_t* A, uint64_t* B)
@@ -102,7 +107,7 @@ __device__ __forceinline__ void rng_prepare(Rng& r)
     const bool urgent = !r.ready && r.idx >= MT_N - RNG_MARGIN;
     if (__any(urgent)) {
         if (!r.ready) {
-            mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
+            mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
             r.ready = 1;
         }
     }
@@ -111,10 +116,10 @@ __device__ __forceinline__ void rng_prepare(Rng& r)
 __device__ __forceinline__ uint64_t rng_raw(Rng& r)
 {
     if (r.idx >= MT_N) {
-        if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
-        r.cur ^= 1;
+        if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+        r.cur   = mt_next(r);
         r.idx   = 0;
-        r.ready = 0;
+        r.ready = r.pre;
         r.pfn   = 0;
     }
     const uint64_t* b = mt_buf(r, r.cur);
@@ -145,10 +150,10 @@ __device__ __forceinline__ void rng_skip(Rng& r, int n)
 {
     while (n > 0) {
         if (r.idx >= MT_N) {
-            if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, r.cur ^ 1));
-            r.cur ^= 1;
+            if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+            r.cur   = mt_next(r);
             r.idx   = 0;
-            r.ready = 0;
+            r.ready = r.pre;
         }
         const int take = (n < MT_N - r.idx) ? n : MT_N - r.idx;
         r.idx += take;
