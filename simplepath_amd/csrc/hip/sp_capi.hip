@@ -1019,9 +1019,17 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             if (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) known_draws = false;
         if (const char* v = std::getenv("SP_CHUNK_REPLAY")) known_draws = known_draws && std::atoi(v) == 0;
         const size_t b_draws  = known_draws ? n_px * spp * 2 : 0;
-        const size_t need_b   = b_hits + b_L + b_snap + b_ctl + b_draws + 4 * 256;
-        double       max_gb   = 96.0;
+        // SP_CHUNK_SPLIT=1: shading split into ck_eval + ck_occl (one shadow ray per sample and
+        // light kept in HBM).  Opt-in: exact, but slower than the fused ck_shade at every shard
+        // size measured (8-way 1374-1366 vs 1498 Mrays/s)
+        size_t b_sray = n_px * spp * (size_t)std::max(1, s->dev.n_lights) * 48;
+        bool   split  = false;
+        if (const char* v = std::getenv("SP_CHUNK_SPLIT")) split = std::atoi(v) != 0 && s->dev.n_lights <= 8;
+        double max_gb = 96.0;
         if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) max_gb = std::atof(v);
+        if ((double)(b_hits + b_L + b_snap + b_ctl + b_draws + b_sray) > max_gb * 1e9) split = false;
+        if (!split) b_sray = 0;
+        const size_t need_b   = b_hits + b_L + b_snap + b_ctl + b_draws + b_sray + 4 * 256;
         if ((double)need_b > max_gb * 1e9)
             return fail(SP_ERR_UNSUPPORTED, "sample-chunk pipeline: buffers exceed SP_CHUNK_MAX_GB (render fewer tiles per call)");
         if (need_b > s->ck_cap) {
@@ -1032,8 +1040,10 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             s->ck_cap = need_b;
         }
         if (!s->ck_ctr) SP_HIP(hipMalloc(&s->ck_ctr, 2 * sizeof(int32_t)));
-        const int    per_cu = spd::chunk_blocks_per_cu(lds_bytes);
-        const int    blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * per_cu, (n_tiles * chunks + 3) / 4));
+        int eval_waves = 4; // ck_eval occupancy (SP_EVAL_WAVES: 2, 3 or 4 waves per SIMD)
+        if (const char* v = std::getenv("SP_EVAL_WAVES")) eval_waves = std::atoi(v);
+        const int per_cu = split ? spd::chunk_eval_blocks_per_cu(eval_waves, (size_t)rs_words * 4) : spd::chunk_blocks_per_cu(lds_bytes);
+        const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * per_cu, (n_tiles * chunks + 3) / 4));
         char*          base = static_cast<char*>(s->ck_buf);
         spd::ChunkArgs a{};
         a.tile_ids  = p->tile_ids ? s->d_tiles : nullptr;
@@ -1049,13 +1059,15 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         a.gens_per_px = gens;
         a.snap_ctl  = reinterpret_cast<uint32_t*>(base + b_hits + b_L + b_snap);
         a.draws     = known_draws ? reinterpret_cast<uint16_t*>(base + b_hits + b_L + b_snap + b_ctl) : nullptr;
+        a.sray      = split ? reinterpret_cast<float4*>(base + b_hits + b_L + b_snap + b_ctl + b_draws) : nullptr;
+        a.n_lights  = s->dev.n_lights;
         a.counter   = s->ck_ctr;
         a.counters  = s->counters;
         a.out       = d_out;
         SP_HIP(hipMemsetAsync(s->ck_ctr, 0, 2 * sizeof(int32_t), stream));
         SP_HIP(hipEventRecord(s->ev0, stream));
-        SP_HIP(spd::chunk_render(s->dev, a, blocks, stream));
-        launches = 4;
+        SP_HIP(spd::chunk_render(s->dev, a, blocks, eval_waves, stream));
+        launches = split ? 5 : 4;
         // camera rays and samples: one per inside pixel and sample (counted here, not on device)
         int64_t inside = 0;
         const int32_t tw = (s->dev.width + 7) / 8;
