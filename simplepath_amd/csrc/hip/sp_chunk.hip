@@ -23,6 +23,12 @@
 // (tests/test_gpu_parity.py).  Camera rays are traced once, and each generation of a stream is
 // twisted once.  HBM per pixel-sample: 16 B hit record + 2 B draw count + 12 B radiance written
 // and read back; per pixel: 2.5 KB per 312 draws of generator store.
+// RNG draw-ahead window (sp_path.hpp Rng): ck_shade reads a generator store that ck_count wrote
+// long before, so every draw is an HBM read; look further ahead than the megakernel does.
+#ifndef SP_CHUNK_RNG_PF
+#define SP_CHUNK_RNG_PF 2
+#endif
+#define SP_RNG_PF SP_CHUNK_RNG_PF
 #include "sp_chunk.hpp"
 #include "sp_mega.hpp"
 
