@@ -991,13 +991,14 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // sp_chunk.hip: camera rays for all (pixel, sample) at once, a per-pixel replay of the
         // stream positions with state snapshots at chunk starts, then every (tile, chunk) shaded
         // in parallel, and the in-order sum.  Chunks per pixel: enough work items to keep the
-        // chip busy when the slowest pixel's chain would otherwise set the frame time.
+        // chip busy when the slowest pixel's chain would otherwise set the frame time (~120K
+        // (tile, chunk) items was best on bunny's 2/4/8-way shards: tools/gpu_sweep_chunks.sh).
         const int    rs_words  = 2 << s->dev.rsqrt_bits;
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         const uint32_t spp    = (uint32_t)p->samples_per_pixel;
         int64_t        chunks = 1;
-        while (chunks < 16 && n_tiles * chunks < 16384) chunks *= 2;
+        while (chunks < 32 && n_tiles * chunks < 120000) chunks *= 2;
         if (const char* v = std::getenv("SP_CHUNKS")) chunks = std::max<int64_t>(1, std::atoll(v));
         chunks = std::min<int64_t>(chunks, spp);
         const uint32_t chunk_len = (uint32_t)((spp + chunks - 1) / chunks);
