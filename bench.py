@@ -25,6 +25,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# oracle/build_ref.sh: the reference's CMake flags (-std=gnu++20 -mfma -mavx2) with -O2 in place of
+# CMake's empty build type (no -O); -ffp-contract=off keeps the -O0 build's IEEE arithmetic
+REF_BUILD = "g++ 11.4 -std=gnu++20 -O2 -ffp-contract=off -mfma -mavx2 (oracle/build_ref.sh)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MT_BYTES_PER_DRAW = 24.0  # 8 B draw read + (2496 B twist read + 2496 B write) / 312
 PIXEL_BYTES = 12.0  # one float3 radiance store per pixel
@@ -60,7 +63,13 @@ def parse():
     ap.add_argument("--integrator", default=None)
     ap.add_argument("--bvh", type=int, default=0, help="0 = SAH, 1 = reference median split")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads for the CPU baseline (0 = this process's CPU share: OMP_NUM_THREADS when set, "
+                         "else os.cpu_count())")
+    ap.add_argument("--parity-seconds", type=float, default=6.0,
+                    help="N > 1: CPU budget for the parity sample of the gathered frame")
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="test hook: spawn the ranks like --gpus N does, join a gloo group, no GPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront", "chunks"])
     ap.add_argument("--sim-world", type=int, default=0,
@@ -75,19 +84,63 @@ def parse():
     return a
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_command(argv, n: int, port: int) -> list:
+    """One process per GPU: torch.distributed.run on this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def self_launch(args) -> int:
+    """`python bench.py --gpus N` without a launcher: start the N ranks as CHILD processes and
+    exit with their status.  Runs before anything touches the GPU (no exec from a GPU process)."""
+    cmd = launch_command(sys.argv[1:], args.gpus, free_port())
+    print(f"bench: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    import subprocess
+    return subprocess.run(cmd).returncode
+
+
+def cpu_share() -> int:
+    """CPUs this process may use: the GPU box gives each GPU a share (OMP_NUM_THREADS), while
+    os.cpu_count() reports the whole machine there."""
+    n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else n
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_selftest:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"launch_selftest": True, "world": dist.get_world_size(), "rank_sum": float(t[0])}),
+                  flush=True)
+        dist.destroy_process_group()
+        return
     import torch
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        world = dist.get_world_size()
     else:
         torch.cuda.set_device(0)
         local = 0
@@ -122,12 +175,17 @@ def main():
         gathered = [torch.zeros_like(out) for _ in range(world)]
         frame = torch.zeros((n_tiles, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
+    gather_ms = []
 
     def step():
         st = sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
                                     pipeline=args.pipeline, stage_timing=True)
         if dist is not None:  # single RCCL gather of the tile buffers at frame end
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             shard.gather_frame(out, n_tiles, rank, world, dist, gathered, frame)
+            e1.record()
+            gather_ms.append((e0, e1))
         return st
 
     for _ in range(args.warmup):
@@ -149,6 +207,9 @@ def main():
     samples = sum(s.samples for s in stats)
     draws = sum(s.rng_draws for s in stats)
     kernel_ms = sum(s.kernel_ms for s in stats) / max(1, len(stats))
+    timed_gathers = gather_ms[-args.steps:] if gather_ms else []
+    g_ms = sum(a.elapsed_time(b) for a, b in timed_gathers) / len(timed_gathers) if timed_gathers else 0.0
+    rank_info = None
     if dist is not None:
         t = torch.tensor([elapsed, float(rays), float(samples), float(draws)], dtype=torch.float64, device=f"cuda:{local}")
         mx = t.clone()
@@ -156,7 +217,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0])
         rays, samples, draws = float(t[1]), float(t[2]), float(t[3])
+        mine = torch.tensor([float(len(my_tiles)), g_ms, kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        rank_info = [{"rank": r, "tiles": int(v[0]), "gather_ms": round(float(v[1]), 3),
+                      "render_ms": round(float(v[2]), 2)} for r, v in enumerate(x.cpu().numpy() for x in every)]
     if rank != 0:
+        dist.barrier()  # rank 0 checks parity of the gathered frame before the group is torn down
         dist.destroy_process_group()
         return
 
@@ -166,13 +233,18 @@ def main():
 
     cpu = None
     parity = None
-    if not args.no_cpu and world == 1:  # the CPU baseline is timed at N=1 only
+    if not args.no_cpu:
         # the reference library logs to stdout (base/Logger.cpp); keep stdout for the JSON line
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            cpu, parity = cpu_baseline(scene, path, integ, args, out if world == 1 else None, my_tiles)
+            if world == 1:  # the CPU baseline is timed at N=1 only
+                cpu, parity = cpu_baseline(scene, path, integ, args, out, my_tiles, args.cpu_seconds)
+            else:  # parity of the GATHERED frame (all ranks' tiles, after the RCCL gather)
+                _, parity = cpu_baseline(scene, path, integ, args, frame, np.arange(n_tiles, dtype=np.int32),
+                                         args.parity_seconds)
+                parity["frame"] = "gathered"
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -202,9 +274,14 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
     }
+    if dist is not None:
+        line["world_size"] = world
+        line["gather_ms"] = round(g_ms, 3)
+        line["ranks"] = rank_info
     print(json.dumps(line), flush=True)
     os.dup2(2, 1)  # exit-time log summaries of the reference library go to stderr
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 
@@ -295,7 +372,7 @@ def _ref_lib():
     return L
 
 
-def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles):
+def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles, budget_s):
     """CPU baseline on a bounded sample of the same frame (whole 8x8 tiles spread over the image,
     same spp and integrator, about --cpu-seconds of work): the reference itself (oracle/_ref,
     kind "reference") when built, else the C oracle (kind "port").  Ray counts come from the
@@ -307,7 +384,7 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles):
     from tests import _oracle
 
     n_tiles = sp.TileScheduler(args.width, args.height).get_num_tiles()
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = args.cpu_threads if args.cpu_threads > 0 else cpu_share()
     rng = np.random.default_rng(1234)
     order = rng.permutation(n_tiles).astype(np.int32)
     ref = _ref_lib()
@@ -329,14 +406,14 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles):
         return out
 
     done, t_used, chunk, tiles_out = [], 0.0, threads, []
-    while t_used < args.cpu_seconds and len(done) < n_tiles:
+    while t_used < budget_s and len(done) < n_tiles:
         ids = np.ascontiguousarray(order[len(done):len(done) + chunk])
         t0 = time.perf_counter()
         tiles_out.append(run(ids))
         dt = time.perf_counter() - t0
         t_used += dt
         done.extend(ids.tolist())
-        if dt < args.cpu_seconds / 8:
+        if dt < budget_s / 8:
             chunk *= 2
     if ref_scene:
         ref.ref_scene_free(ref_scene)
@@ -347,7 +424,8 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles):
            "sample": f"{len(done)} random 8x8 tiles of the same frame @ {args.spp} spp ({st['samples']} samples, "
                      f"{t_used:.1f} s, " + ("oracle/_ref/libsp_ref.so = reference sources" if ref is not None
                                              else "oracle liboracle_glibc.so") + ")",
-           "msamples_per_s": round(st["samples"] / t_used / 1e6, 5)}
+           "msamples_per_s": round(st["samples"] / t_used / 1e6, 5), "host_cores": os.cpu_count(),
+           "build": REF_BUILD if ref is not None else "oracle/Makefile: gcc -O2 -mavx2 -mfma -ffp-contract=off"}
     parity = {"vs": kind, "tiles": len(done)}
     if ref is not None:
         parity["oracle_bitexact_vs_reference"] = bool(np.array_equal(orc.view(np.uint32), base.view(np.uint32)))

@@ -16,6 +16,8 @@
  *   sp_scene_get_desc                     the primitive / light / material / camera state
  *                                         held by base/Scene.h:99-105 (flattened, host memory)
  *   sp_scene_upload                       (no reference counterpart: HBM residency)
+ *   sp_scene_bvh_build_info               base/Scene.h:59 Scene ctor's BVHAccelerator build
+ *                                         (shapes/BVHAccelerator.h:173), host only: statistics
  *   sp_render_tiles                       main.cpp:77-107 `render_thread`: for each scheduled
  *                                         tile, for each pixel, num_pixel_samples x
  *                                         `integrator.integrate(camera.generate_ray(...))`,
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 2
+#define SP_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------------- */
 enum {
@@ -207,8 +209,17 @@ typedef struct sp_render_stats {
     float    stage_ms[4];     /* with SP_RENDER_STAGE_TIMING, wavefront: [init+resolve, primary,   */
                               /* shade, shadow] of part 0 summed over launches; megakernel: [0]   */
     int32_t  parts;           /* wavefront: concurrent parts (streams); part 0 holds ceil(tiles/2) */
-    int32_t  reserved;
+    int32_t  stack_depth;     /* traversal-stack entries per lane the BVH walks needed (ABI 3)      */
 } sp_render_stats;
+
+/* BVH statistics (sp_scene_bvh_build_info).  depth = levels below the root of the binary BVH
+ * (the reference's recursive BVHAccelerator walk, shapes/BVHAccelerator.h:62-77, nests this deep);
+ * wide_depth = depth of the 8-wide any-hit BVH (SAH only, else 0); light_depth = the light
+ * accelerator's; stack_depth = traversal-stack entries per lane a render needs. */
+typedef struct sp_bvh_info {
+    int32_t depth, wide_depth, light_depth, stack_depth;
+    int64_t nodes, slots;
+} sp_bvh_info;
 
 /* ---- API ------------------------------------------------------------------------------ */
 typedef struct sp_scene sp_scene;
@@ -243,6 +254,9 @@ int  sp_render_tiles_host(sp_scene* scene, const sp_render_params* params, float
                           sp_render_stats* stats);
 /* BVH statistics of the uploaded scene (depth, node count, primitive slots). */
 int  sp_scene_bvh_info(const sp_scene* scene, int32_t* depth, int64_t* nodes, int64_t* slots);
+/* Host only (no device needed): build the geometry BVH sp_scene_upload would build for bvh_mode
+ * and report its statistics; nothing is uploaded. */
+int  sp_scene_bvh_build_info(const sp_scene* scene, int32_t bvh_mode, sp_bvh_info* out);
 /* Scatter tile-packed radiance (host memory) into a row-major width x height x 3 image. */
 int  sp_tiles_to_image(int32_t width, int32_t height, const int32_t* tile_ids, int64_t num_tiles,
                        const float* tiles, float* image);

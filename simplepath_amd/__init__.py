@@ -49,6 +49,7 @@ class RenderStats:
     primary_hits: int = 0
     stage_ms: tuple = (0.0, 0.0, 0.0, 0.0)
     parts: int = 1
+    stack_depth: int = 0
 
 
 class Scene:
@@ -115,6 +116,12 @@ class Scene:
         check(lib().sp_scene_bvh_info(self._h, C.byref(d), C.byref(n), C.byref(s)))
         return {"depth": d.value, "nodes": n.value, "slots": s.value}
 
+    def bvh_build_info(self, bvh_mode: int = 0) -> dict:
+        """Host-only BVH build statistics (no device): what upload(bvh_mode) would build."""
+        i = _abi.sp_bvh_info()
+        check(lib().sp_scene_bvh_build_info(self._h, bvh_mode, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in _abi.sp_bvh_info._fields_}
+
 
 class TileScheduler:
     """base/TileScheduler.h:18 -- tiles of k_tile_dimension^2 pixels over the image extents."""
@@ -178,7 +185,7 @@ def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeli
 
 def _stats(s: _abi.sp_render_stats) -> RenderStats:
     return RenderStats(s.rays, s.shadow_rays, s.samples, s.rng_draws, s.kernel_ms, s.pipeline, s.launches,
-                       s.primary_hits, tuple(s.stage_ms), s.parts)
+                       s.primary_hits, tuple(s.stage_ms), s.parts, s.stack_depth)
 
 
 def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Optional[Sequence[int]] = None,

@@ -99,7 +99,12 @@ class sp_render_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
                 ("rng_draws", C.c_uint64), ("kernel_ms", C.c_float), ("pipeline", C.c_int32),
                 ("launches", C.c_int32), ("primary_hits", C.c_uint64), ("stage_ms", C.c_float * 4),
-                ("parts", C.c_int32), ("reserved", C.c_int32)]
+                ("parts", C.c_int32), ("stack_depth", C.c_int32)]
+
+
+class sp_bvh_info(C.Structure):
+    _fields_ = [("depth", C.c_int32), ("wide_depth", C.c_int32), ("light_depth", C.c_int32),
+                ("stack_depth", C.c_int32), ("nodes", C.c_int64), ("slots", C.c_int64)]
 
 
 # Every symbol declared in include/simplepath_hip.h, with its ctypes signature.
@@ -121,6 +126,7 @@ SIGNATURES = {
     "sp_render_tiles_host": (C.c_int, [C.c_void_p, C.POINTER(sp_render_params), C.POINTER(C.c_float),
                                        C.POINTER(sp_render_stats)]),
     "sp_scene_bvh_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "sp_scene_bvh_build_info": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(sp_bvh_info)]),
     "sp_tiles_to_image": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int64,
                                     C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "sp_write_pfm": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_float)]),

@@ -14,6 +14,14 @@
 // the host libm over all 2^32 inputs (powf: structured + random pairs) by
 // tests/test_libm_exact.py.  The same source is compiled for the host and for gfx950 with
 // explicit fma() and no contraction, so the host verification carries over to the device.
+//
+// Attribution: the algorithms, polynomial coefficients and tables restated here are those of
+// the GNU C Library 2.35 (glibc, LGPL-2.1-or-later), whose expf/logf/powf/sinf/cosf come from
+// Arm's optimized-routines (Copyright (c) 2017-2018 Arm Ltd., MIT / LGPL as distributed with
+// glibc) and whose erff/acosf/atanf/atan2f are Sun Microsystems' fdlibm (Copyright (C) 1993 Sun
+// Microsystems, Inc.: "Permission to use, copy, modify, and distribute this software is freely
+// granted, provided that this notice is preserved").  The table values in sp_glibc_data.h are
+// read from the system libm.so.6 by tools/extract_glibc_libm.py.
 #pragma once
 #include "sp_math.h"
 #include "sp_glibc_data.h"

@@ -58,111 +58,6 @@ sph::PrimBounds tri_bounds(const sph::Scene& s, int t)
     return b;
 }
 
-// Pair-node copy of a binary BVH: pair k = the two children of the k-th internal node (DFS
-// preorder), 16 floats {lo0, hi0, lo1, hi1, ref0, ref1, split axis, 0} (sp_path.hpp).
-std::vector<float4> pair_nodes(const sph::Bvh& bvh)
-{
-    const auto&           bn = bvh.nodes;
-    std::vector<uint32_t> pair_of(bn.size(), spd::PNONE);
-    uint32_t              np = 0;
-    std::vector<uint32_t> todo{ 0 };
-    while (!todo.empty()) { // preorder numbering of internal nodes
-        const uint32_t i = todo.back();
-        todo.pop_back();
-        if (bn[i].b & sph::BVH_LEAF) continue;
-        pair_of[i] = np++;
-        todo.push_back(bn[i].b);
-        todo.push_back(bn[i].a & sph::BVH_CHILD_MASK);
-    }
-    auto ref_of = [&](uint32_t i) -> uint32_t {
-        if (bn[i].b & sph::BVH_LEAF) {
-            const uint32_t cnt = bn[i].b & ~sph::BVH_LEAF;
-            if (cnt > 7 || bn[i].a > 0x0fffffffu) throw std::runtime_error("leaf does not fit a pair reference");
-            return spd::PLEAF | (cnt << 28) | bn[i].a;
-        }
-        return pair_of[i];
-    };
-    auto u2f = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
-    std::vector<float4> out;
-    if (bn[0].b & sph::BVH_LEAF) { // single leaf: one pair with an empty second child
-        const auto& r = bn[0];
-        out.push_back(make_float4(r.lo[0], r.lo[1], r.lo[2], r.hi[0]));
-        out.push_back(make_float4(r.hi[1], r.hi[2], 0.0f, 0.0f));
-        out.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        out.push_back(make_float4(u2f(ref_of(0)), u2f(spd::PNONE), u2f(0), 0.0f));
-        return out;
-    }
-    out.resize((size_t)np * 4);
-    for (size_t i = 0; i < bn.size(); ++i) {
-        if (pair_of[i] == spd::PNONE) continue;
-        const auto&    n = bn[i];
-        const uint32_t l = n.a & sph::BVH_CHILD_MASK, r = n.b;
-        const auto&    L = bn[l];
-        const auto&    R = bn[r];
-        float4*        q = &out[(size_t)pair_of[i] * 4];
-        q[0] = make_float4(L.lo[0], L.lo[1], L.lo[2], L.hi[0]);
-        q[1] = make_float4(L.hi[1], L.hi[2], R.lo[0], R.lo[1]);
-        q[2] = make_float4(R.lo[2], R.hi[0], R.hi[1], R.hi[2]);
-        q[3] = make_float4(u2f(ref_of(l)), u2f(ref_of(r)), u2f(n.a >> sph::BVH_AXIS_SHIFT), 0.0f);
-    }
-    return out;
-}
-
-// 16-byte quantised copy of a binary SAH BVH (sp_path.hpp qnode_*): boxes as 16-bit offsets
-// from the root box on a per-axis grid, rounded outward so every decoded box (decoded on the
-// device as fmaf(q, scale, origin), here with the same fused operation) contains its exact box;
-// siblings adjacent, so a node is {lo.xyz, hi.xyz as u16, meta} with meta = first child | axis
-// << 29, or QLEAF | count << 28 | first slot.
-std::vector<uint4> quantized_nodes(const sph::Bvh& bvh, float origin[3], float scale[3])
-{
-    const auto& bn = bvh.nodes;
-    for (int a = 0; a < 3; ++a) {
-        const float lo = bn[0].lo[a], hi = bn[0].hi[a];
-        float       s  = (hi > lo) ? (hi - lo) / 65535.0f : 1e-30f;
-        while (std::fmaf(65535.0f, s, lo) < hi) s = std::nextafterf(s, INFINITY);
-        origin[a] = lo;
-        scale[a]  = s;
-    }
-    auto qlo = [&](int a, float v) -> uint32_t {
-        double   f = std::floor(((double)v - origin[a]) / scale[a]);
-        uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, f));
-        while (q > 0 && std::fmaf((float)q, scale[a], origin[a]) > v) --q;
-        return q;
-    };
-    auto qhi = [&](int a, float v) -> uint32_t {
-        double   f = std::ceil(((double)v - origin[a]) / scale[a]);
-        uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, f));
-        while (q < 65535 && std::fmaf((float)q, scale[a], origin[a]) < v) ++q;
-        return q;
-    };
-    std::vector<uint4> out(bn.size());
-    std::vector<std::pair<uint32_t, uint32_t>> todo{ { 0u, 0u } }; // (binary node, output slot)
-    uint32_t next = 1;
-    while (!todo.empty()) {
-        const auto [i, k] = todo.back();
-        todo.pop_back();
-        const auto& n = bn[i];
-        uint32_t    q[6];
-        for (int a = 0; a < 3; ++a) { q[a] = qlo(a, n.lo[a]); q[3 + a] = qhi(a, n.hi[a]); }
-        uint32_t meta;
-        if (n.b & sph::BVH_LEAF) {
-            const uint32_t cnt = n.b & ~sph::BVH_LEAF;
-            if (cnt > 7 || n.a > 0x0fffffffu) throw std::runtime_error("leaf does not fit a quantized node");
-            meta = spd::QLEAF | (cnt << 28) | n.a;
-        } else {
-            const uint32_t first = next;
-            next += 2;
-            if (first > 0x1fffffffu) throw std::runtime_error("too many nodes for a quantized BVH");
-            meta = first | ((n.a >> sph::BVH_AXIS_SHIFT) << 29);
-            todo.push_back({ n.b, first + 1 });
-            todo.push_back({ n.a & sph::BVH_CHILD_MASK, first });
-        }
-        out[k] = make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), meta);
-    }
-    out.resize(next);
-    return out;
-}
-
 spm::aff from_desc(const sp_affine& d)
 {
     spm::aff a;
@@ -198,6 +93,72 @@ sph::PrimBounds sphere_bounds(const spm::aff& o2w)
         }
     }
     return b;
+}
+
+// Scene ctor partition (base/Scene.h:29: bounded primitives first, planes after, libstdc++
+// std::partition order) and the BVH over the bounded part: the reference's median split
+// (bvh_mode 1, shapes/BVHAccelerator.h:173) or SAH.
+sph::Bvh geometry_bvh(const sph::Scene& h, int bvh_mode, std::vector<int32_t>& prims, size_t& part)
+{
+    prims.resize(h.prim_kind.size());
+    for (size_t i = 0; i < prims.size(); ++i) prims[i] = (int32_t)i;
+    part = sph::stl_partition(prims, 0, prims.size(), [&](int32_t p) { return h.prim_kind[p] != SP_PRIM_PLANE; });
+    std::vector<sph::PrimBounds> bounds;
+    bounds.reserve(part);
+    for (size_t i = 0; i < part; ++i) {
+        const int32_t p = prims[i];
+        if (h.prim_kind[p] == SP_PRIM_TRIANGLE) bounds.push_back(tri_bounds(h, h.prim_index[p]));
+        else bounds.push_back(sphere_bounds(from_desc(h.shapes[h.prim_index[p]].object_to_world)));
+    }
+    // SAH leaf size limit (SP_SAH_LEAF tuning knob, 1..4: 8 collapsed leaves of a wide node must
+    // fit its 5-bit leaf offsets; the sweep in DESIGN.md §4 found 4 best)
+    int sah_leaf = 4;
+    if (const char* v = std::getenv("SP_SAH_LEAF")) sah_leaf = std::max(1, std::min(4, std::atoi(v)));
+    return (bvh_mode == 1) ? sph::build_bvh_reference(bounds) : sph::build_bvh_sah(bounds, sah_leaf);
+}
+
+// SAH scenes get the 8-wide quantised BVH for any-hit queries (SP_WIDE=0 keeps the binary walk)
+bool wide_enabled(int bvh_mode)
+{
+    const char* v = std::getenv("SP_WIDE");
+    return bvh_mode != 1 && (v ? std::atoi(v) != 0 : true);
+}
+
+// Traversal-stack budget: a BVH deeper than this many levels is walked without a stack (parent
+// links, sp_path.hpp bvh_next) instead of failing.  96 entries x 4 B x 64 lanes x 4 waves = 96 KB
+// of LDS, which leaves room for the 16 KB RSQRTSS table and a second block per CU.
+// SP_STACKLESS=1 forces the stackless walk (tests), SP_STACK_MAX=<levels> moves the threshold.
+bool stackless_for(int depth)
+{
+    if (const char* v = std::getenv("SP_STACKLESS"))
+        if (std::atoi(v) != 0) return true;
+    int max_levels = 96;
+    if (const char* v = std::getenv("SP_STACK_MAX")) max_levels = std::max(1, std::atoi(v));
+    return depth + 1 > max_levels;
+}
+
+// Scene ctor's light accelerator (base/Scene.h:29): sphere lights first (libstdc++
+// std::partition order), the reference BVH over them; the rest are unbounded
+sph::Bvh light_bvh(const sph::Scene& h, std::vector<int32_t>& lids, size_t& lpart)
+{
+    lids.resize(h.lights.size());
+    for (size_t i = 0; i < lids.size(); ++i) lids[i] = (int32_t)i;
+    lpart = sph::stl_partition(lids, 0, lids.size(), [&](int32_t i) { return h.lights[i].kind == SP_LIGHT_SPHERE; });
+    std::vector<sph::PrimBounds> lb;
+    for (size_t i = 0; i < lpart; ++i) lb.push_back(sphere_bounds(from_desc(h.lights[lids[i]].object_to_world)));
+    return sph::build_bvh_reference(lb);
+}
+
+// parent[i] of every node of a binary BVH (the root is its own parent)
+std::vector<uint32_t> parent_links(const std::vector<sph::BvhNode>& nodes)
+{
+    std::vector<uint32_t> par(nodes.size(), 0u);
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        if (nodes[i].b & sph::BVH_LEAF) continue;
+        par[nodes[i].a & sph::BVH_CHILD_MASK] = (uint32_t)i;
+        par[nodes[i].b]                       = (uint32_t)i;
+    }
+    return par;
 }
 
 struct DevBuf {
@@ -538,12 +499,10 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
     }
 
     // ---- geometry: Scene ctor partition (base/Scene.h:29) then BVH over the bounded part
-    std::vector<int32_t> prims(h.prim_kind.size());
-    for (size_t i = 0; i < prims.size(); ++i) prims[i] = (int32_t)i;
-    const size_t part = sph::stl_partition(prims, 0, prims.size(),
-                                           [&](int32_t p) { return h.prim_kind[p] != SP_PRIM_PLANE; });
-    std::vector<sph::PrimBounds> bounds;
-    std::vector<spd::Shape>      shapes;
+    std::vector<int32_t> prims;
+    size_t               part = 0;
+    const sph::Bvh       bvh  = geometry_bvh(h, bvh_mode, prims, part);
+    std::vector<spd::Shape> shapes;
     for (auto& sh : h.shapes) {
         spd::Shape x{};
         x.o2w      = from_desc(sh.object_to_world);
@@ -553,18 +512,8 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
         x.kind     = sh.kind;
         shapes.push_back(x);
     }
-    for (size_t i = 0; i < part; ++i) {
-        const int32_t p = prims[i];
-        if (h.prim_kind[p] == SP_PRIM_TRIANGLE) bounds.push_back(tri_bounds(h, h.prim_index[p]));
-        else bounds.push_back(sphere_bounds(shapes[h.prim_index[p]].o2w));
-    }
     std::vector<int32_t> unbounded;
     for (size_t i = part; i < prims.size(); ++i) unbounded.push_back(h.prim_index[prims[i]]);
-    // SAH leaf size limit (SP_SAH_LEAF tuning knob, 1..4: 8 collapsed leaves of a wide node must
-    // fit its 5-bit leaf offsets; the sweep in DESIGN.md §4 found 4 best)
-    int sah_leaf = 4;
-    if (const char* v = std::getenv("SP_SAH_LEAF")) sah_leaf = std::max(1, std::min(4, std::atoi(v)));
-    const sph::Bvh bvh = (bvh_mode == 1) ? sph::build_bvh_reference(bounds) : sph::build_bvh_sah(bounds, sah_leaf);
     std::vector<float4>   slot_tri(bvh.prim_order.size() * 3);
     std::vector<uint32_t> slot_code(bvh.prim_order.size());
     for (size_t sl = 0; sl < bvh.prim_order.size(); ++sl) {
@@ -585,33 +534,6 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
     std::vector<spd::Node> nodes(bvh.nodes.size());
     static_assert(sizeof(spd::Node) == sizeof(sph::BvhNode), "node layout");
     std::memcpy(nodes.data(), bvh.nodes.data(), nodes.size() * sizeof(spd::Node));
-    std::vector<float4> pairs; // SAH: pair-node copy (sp_path.hpp pair_closest / pair_any)
-    if (bvh_mode != 1 && !nodes.empty()) {
-        // opt-in (SP_PAIRS=1): the bunny frame is bound by vector-L1 accesses, which pair nodes
-        // do not reduce (same bytes per box), and their t0 stack halves the LDS occupancy
-        const bool use_pairs = std::getenv("SP_PAIRS") && std::atoi(std::getenv("SP_PAIRS")) != 0;
-        if (use_pairs) pairs = pair_nodes(bvh);
-    }
-    // SAH: 8-wide quantised BVH (default; SP_WIDE=0 keeps the binary walk)
-    sph::WideBvh        wide;
-    std::vector<float4> wslot_tri;
-    {
-        const char* v      = std::getenv("SP_WIDE");
-        const bool  use_w  = v ? std::atoi(v) != 0 : true;
-        if (use_w && bvh_mode != 1 && !nodes.empty() && pairs.empty()) {
-            wide = sph::build_wide(bvh);
-            wslot_tri.resize(wide.slot_of.size() * 3);
-            for (size_t i = 0; i < wide.slot_of.size(); ++i)
-                for (int k = 0; k < 3; ++k) wslot_tri[3 * i + k] = slot_tri[3 * (size_t)wide.slot_of[i] + k];
-        }
-    }
-    std::vector<uint4> qnodes; // SAH: 16-byte quantised nodes (opt-in SP_QNODES=1: slower on the bunny frame)
-    float              qo[3] = { 0, 0, 0 }, qs[3] = { 0, 0, 0 };
-    if (bvh_mode != 1 && !nodes.empty() && pairs.empty()) {
-        const bool use_q = std::getenv("SP_QNODES") && std::atoi(std::getenv("SP_QNODES")) != 0;
-        if (use_q) qnodes = quantized_nodes(bvh, qo, qs);
-    }
-
     // ---- lights: Scene::m_lights order + accelerator (partition by boundedness)
     std::vector<spd::Light> lights;
     for (auto& l : h.lights) {
@@ -624,17 +546,26 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
         x.nrm      = from_desc(l.normal_to_world);
         lights.push_back(x);
     }
-    std::vector<int32_t> lids(lights.size());
-    for (size_t i = 0; i < lids.size(); ++i) lids[i] = (int32_t)i;
-    const size_t lpart = sph::stl_partition(lids, 0, lids.size(), [&](int32_t i) { return lights[i].kind == SP_LIGHT_SPHERE; });
-    std::vector<sph::PrimBounds> lbounds;
-    for (size_t i = 0; i < lpart; ++i) lbounds.push_back(sphere_bounds(lights[lids[i]].o2w));
+    std::vector<int32_t> lids;
+    size_t               lpart = 0;
+    const sph::Bvh       lbvh  = light_bvh(h, lids, lpart);
     std::vector<int32_t> unbounded_lights(lids.begin() + (long)lpart, lids.end());
-    const sph::Bvh lbvh = sph::build_bvh_reference(lbounds);
     std::vector<uint32_t> light_slot(lbvh.prim_order.size());
     for (size_t sl = 0; sl < light_slot.size(); ++sl) light_slot[sl] = (uint32_t)lids[lbvh.prim_order[sl]];
     std::vector<spd::Node> lnodes(lbvh.nodes.size());
     std::memcpy(lnodes.data(), lbvh.nodes.data(), lnodes.size() * sizeof(spd::Node));
+
+    // SAH: 8-wide quantised BVH for any-hit queries (SP_WIDE=0 keeps the binary walk); a
+    // stackless scene walks the binary BVH only
+    const bool          stackless = stackless_for(std::max(bvh.max_depth, lbvh.max_depth));
+    sph::WideBvh        wide;
+    std::vector<float4> wslot_tri;
+    if (wide_enabled(bvh_mode) && !nodes.empty() && !stackless) {
+        wide = sph::build_wide(bvh);
+        wslot_tri.resize(wide.slot_of.size() * 3);
+        for (size_t i = 0; i < wide.slot_of.size(); ++i)
+            for (int k = 0; k < 3; ++k) wslot_tri[3 * i + k] = slot_tri[3 * (size_t)wide.slot_of[i] + k];
+    }
 
     // ---- upload
     int rc2 = SP_OK;
@@ -652,10 +583,6 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
     up(unbounded, &d.unbounded);
     d.n_nodes = (int)nodes.size();
     up(nodes, &d.nodes);
-    d.pairs = nullptr;
-    if (!pairs.empty()) up(pairs, &d.pairs);
-    d.qnodes = nullptr;
-    if (!qnodes.empty()) up(qnodes, &d.qnodes);
     d.wnodes    = nullptr;
     d.wslot_tri = nullptr;
     if (!wide.words.empty()) {
@@ -664,7 +591,6 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
         up(wn, &d.wnodes);
         up(wslot_tri, &d.wslot_tri);
     }
-    for (int a = 0; a < 3; ++a) { d.qorigin[a] = qo[a]; d.qscale[a] = qs[a]; }
     up(slot_tri, &d.slot_tri);
     up(slot_code, &d.slot_code);
     std::vector<float> nrm(h.normals.size() * 3);
@@ -721,18 +647,22 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
     s->geom_nodes  = nodes.size();
     s->geom_slots  = slot_code.size();
     // Any-hit queries walk the 8-wide BVH; closest-hit queries keep the binary near-first walk
-    // unless SP_WIDE_CLOSEST=1 (coherent camera rays: binary 0.48 vs wide 0.69 ms per primary
-    // launch on the bunny frame, while shadow rays gain 0.82 -> 0.53 ms).
-    d.wide_closest = 0;
-    if (const char* v = std::getenv("SP_WIDE_CLOSEST")) d.wide_closest = (!wide.words.empty() && std::atoi(v) != 0) ? 1 : 0;
-    d.stack_depth  = std::max(d.wide_closest ? wide.depth : bvh.max_depth, std::max(wide.depth, lbvh.max_depth)) + 1;
-    d.stack_words  = d.stack_depth * (d.pairs ? 2 : 1);
-    // Wave-coherent traversal (sp_packet.hpp) is opt-in (SP_PACKET=1): on the bunny frame the
-    // per-lane walk is faster (profiles/r01: packet steps are one dependent fetch per wave).
-    d.packet       = 0;
-    d.ordered      = bvh_mode == 1 ? 0 : 1;       // reference order is part of the bit-exact contract
-    if (const char* v = std::getenv("SP_PACKET")) d.packet = (d.stack_depth <= 64) && std::atoi(v) != 0;
-    if (const char* v = std::getenv("SP_ORDERED")) d.ordered = d.ordered && std::atoi(v) != 0;
+    // (coherent camera rays: binary 0.48 vs wide 0.69 ms per primary launch on the bunny frame,
+    // while shadow rays gain 0.82 -> 0.53 ms).
+    d.ordered     = bvh_mode == 1 ? 0 : 1; // reference order is part of the bit-exact contract
+    d.stack_depth = std::max(bvh.max_depth, std::max(wide.depth, lbvh.max_depth)) + 1;
+    d.stackless   = stackless ? 1 : 0;
+    d.parents       = nullptr;
+    d.light_parents = nullptr;
+    if (d.stackless) { // deeper than the LDS budget: parent links instead of a stack
+        std::vector<uint32_t> par  = parent_links(bvh.nodes);
+        std::vector<uint32_t> lpar = parent_links(lbvh.nodes);
+        up(par, &d.parents);
+        up(lpar, &d.light_parents);
+        if (rc2 != SP_OK) return rc2;
+        d.stack_depth = 0;
+    }
+    d.stack_words = d.stack_depth;
     SP_HIP(hipMalloc(&s->tile_counter, sizeof(int32_t)));
     SP_HIP(hipMalloc(&s->counters, 8 * sizeof(unsigned long long)));
     SP_HIP(hipEventCreate(&s->ev0));
@@ -1192,6 +1122,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         stats->launches    = launches;
         stats->primary_hits = c[4];
         stats->parts        = parts_used;
+        stats->stack_depth  = s->dev.stack_depth;
         if (pipeline == SP_PIPELINE_MEGAKERNEL && timing) stage[0] = ms;
         for (int k = 0; k < 4; ++k) stats->stage_ms[k] = stage[k];
     }
@@ -1252,6 +1183,31 @@ int sp_write_pfm(const char* path, int32_t width, int32_t height, const float* i
         std::fwrite(image + (size_t)j * width * 3, sizeof(float), (size_t)width * 3, f);
     std::fclose(f);
     return SP_OK;
+}
+
+int sp_scene_bvh_build_info(const sp_scene* s, int32_t bvh_mode, sp_bvh_info* out)
+{
+    if (!s || !out) return fail(SP_ERR_ARG, "null argument");
+    if (bvh_mode != 0 && bvh_mode != 1) return fail(SP_ERR_ARG, "bvh_mode must be 0 (SAH) or 1 (reference)");
+    try {
+        const sph::Scene&    h = *s->host;
+        std::vector<int32_t> prims;
+        size_t               part = 0;
+        const sph::Bvh       bvh  = geometry_bvh(h, bvh_mode, prims, part);
+        *out                      = sp_bvh_info{};
+        out->depth                = bvh.max_depth;
+        out->nodes                = (int64_t)bvh.nodes.size();
+        out->slots                = (int64_t)bvh.prim_order.size();
+        std::vector<int32_t> lids;
+        size_t               lpart = 0;
+        out->light_depth           = light_bvh(h, lids, lpart).max_depth;
+        const bool stackless       = stackless_for(std::max(out->depth, out->light_depth));
+        if (wide_enabled(bvh_mode) && !bvh.nodes.empty() && !stackless) out->wide_depth = sph::build_wide(bvh).depth;
+        out->stack_depth = stackless ? 0 : std::max(out->depth, std::max(out->wide_depth, out->light_depth)) + 1;
+        return SP_OK;
+    } catch (const std::exception& e) {
+        return fail(SP_ERR_UNSUPPORTED, std::string("BVH build failed: ") + e.what());
+    }
 }
 
 int sp_scene_bvh_info(const sp_scene* s, int32_t* depth, int64_t* nodes, int64_t* slots)

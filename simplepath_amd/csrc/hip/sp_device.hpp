@@ -25,9 +25,6 @@ constexpr uint32_t CODE_SHIFT = 30;
 constexpr uint32_t CODE_MASK  = (1u << CODE_SHIFT) - 1u;
 constexpr uint32_t AXIS_SHIFT = 30;                      // sp_host.hpp BVH_AXIS_SHIFT
 constexpr uint32_t CHILD_MASK = (1u << AXIS_SHIFT) - 1u;
-constexpr uint32_t PLEAF      = 0x80000000u; // pair-node child reference: leaf flag
-constexpr uint32_t PNONE      = 0xffffffffu; // pair-node child reference: no child
-constexpr uint32_t QLEAF      = 0x80000000u; // quantised node meta: leaf flag
 
 struct Node {
     float    lo[3];
@@ -86,9 +83,6 @@ struct Scene {
     const int32_t*  unbounded; // shape indices (planes), reference partition order
     int             n_nodes;
     const Node*     nodes;
-    const float4*   pairs;     // pair-node copy of an SAH BVH (sp_path.hpp), nullptr otherwise
-    const uint4*    qnodes;    // 16-byte quantised copy of an SAH BVH (sp_path.hpp), nullptr otherwise
-    float           qorigin[3], qscale[3];
     const uint4*    wnodes;    // 8-wide BVH (sp_host.hpp WideBvh), 5 per node; nullptr = binary walk
     const float4*   wslot_tri; // 3 per wide-BVH primitive slot
     const float4*   slot_tri;  // 3 per slot
@@ -113,11 +107,14 @@ struct Scene {
     const uint32_t* rsqrt_entries; // 2 << rsqrt_bits
     int32_t         rsqrt_bits;
     uint32_t        rsqrt_zero, rsqrt_denorm;
-    int             stack_depth;   // LDS traversal stack entries per lane
-    int             stack_words;   // LDS words per lane (2 per entry for the pair-node walk)
-    int             packet;        // 1: BVHs shallow enough for the wave-coherent walk (sp_packet.hpp)
+    int             stack_depth;   // LDS traversal stack entries per lane (0 when stackless)
+    int             stack_words;   // LDS words per lane
     int             ordered;       // 1: SAH BVH -- visit the near child (split axis, ray sign) first
-    int             wide_closest;  // 1: closest-hit queries walk the 8-wide BVH too (any-hit always does)
+    // BVHs too deep for the LDS stack budget: binary walks climb parent links instead of popping
+    // a stack (same visiting order and box tests; sp_path.hpp bvh_next)
+    int             stackless;
+    const uint32_t* parents;       // parent of each geometry node (root: itself)
+    const uint32_t* light_parents; // parent of each light-BVH node
 };
 
 struct RenderArgs {

@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(256) tile_cost_kernel(Scene sc, const int32_t*
         Ray ray;
         ray.o = sc.camera.p;
         ray.d = normalize(add(add(scale((float)px + 0.5f, sc.camera.vx), scale((float)py + 0.5f, sc.camera.vy)), sc.camera.vz), q);
-        const Hit h = scene_intersect<false>(sc, ray, k_ray_epsilon, k_infinite, st);
+        const Hit h = scene_intersect(sc, ray, k_ray_epsilon, k_infinite, st);
         if (h.code != 0xffffffffu) {
             const Isect is = finish_hit(sc, h, ray, q);
             Material    m  = sc.materials[is.material];

@@ -380,16 +380,63 @@ __device__ __forceinline__ bool near_is_second(uint32_t a, const f3& d)
     return da < 0.0f;
 }
 
+// Depth-first walk of a binary BVH in the reference's recursion order: a node's second child is
+// deferred while the first child's subtree is walked, and box-tested (against the limits current
+// then) when the walk comes back to it.  The deferred children live on the LDS stack, or -- for
+// BVHs deeper than the LDS budget (Scene::stackless) -- are found again by climbing parent links
+// from the finished subtree to the first ancestor entered through its first child: the same
+// nodes, in the same order, with the same box tests, and no per-lane memory at all (a degenerate
+// median-split tree can nest thousands of levels, like the reference's recursion).
+struct BinWalk {
+    Stack           st;
+    int             sp;
+    const Node*     nodes;
+    const uint32_t* parents; // non-null: stackless
+    bool            ordered; // SAH near-first order
+};
+__device__ __forceinline__ BinWalk bin_walk(Stack st, const Node* nodes, const uint32_t* parents, bool stackless,
+                                            bool ordered)
+{
+    return BinWalk{ st, 0, nodes, stackless ? parents : nullptr, ordered };
+}
+__device__ __forceinline__ void children_in_order(const BinWalk& w, const Node& n, const f3& d, uint32_t& first,
+                                                  uint32_t& second)
+{
+    first  = n.a & CHILD_MASK;
+    second = n.b;
+    if (w.ordered && near_is_second(n.a, d)) { const uint32_t t = first; first = second; second = t; }
+}
+__device__ __forceinline__ void walk_defer(BinWalk& w, uint32_t second)
+{
+    if (w.parents) return;
+    w.st.s[w.sp * 64 + w.st.lane] = second;
+    ++w.sp;
+}
+// The next deferred node after the subtree at `cur` is finished; false when the walk is done.
+__device__ __forceinline__ bool walk_next(BinWalk& w, const f3& d, uint32_t& cur)
+{
+    if (!w.parents) {
+        if (w.sp == 0) return false;
+        --w.sp;
+        cur = w.st.s[w.sp * 64 + w.st.lane];
+        return true;
+    }
+    while (cur != 0) {
+        const uint32_t p = w.parents[cur];
+        uint32_t       first, second;
+        children_in_order(w, w.nodes[p], d, first, second);
+        if (cur == first) {
+            cur = second;
+            return true;
+        }
+        cur = p;
+    }
+    return false;
+}
 
-// ------------------------------------------------------------------------------ pair-node BVH
-// SAH builds are also stored as "pair nodes" (16 floats): the boxes of BOTH children of an
-// internal binary node plus their references, so one 64-byte fetch tests two boxes and a culled
-// child costs no fetch at all.  ref: internal = pair index; leaf = PLEAF | count << 28 | first
-// slot; PNONE = no child (single-leaf tree).  The closest-hit walk keeps each deferred child's
-// entry distance t0 on the stack and drops it on pop when t0 > current t_max -- exactly the box
-// test the deferred child would fail at that time (t_min unchanged, t_max only shrinks).
 
-__device__ __forceinline__ bool pair_box(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r,
+// Slab test of one box with its entry distance (math/BBox.h:254 operation order).
+__device__ __forceinline__ bool slab_box(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r,
                                          const f3& inv, float tmin, float tmax, float& t0_out)
 {
     float t0 = tmin, t1 = tmax; // same operation order as box_hit (math/BBox.h:254)
@@ -418,97 +465,6 @@ __device__ __forceinline__ bool pair_box(float lx, float ly, float lz, float hx,
     return true;
 }
 
-struct PairHits {
-    uint32_t near_ref, far_ref;
-    float    far_t0;
-    int      n; // 0, 1 (near_ref) or 2 (near_ref first, far_ref deferred)
-};
-__device__ __forceinline__ PairHits pair_visit(const Scene& sc, uint32_t ref, const Ray& ray, const f3& inv, float tmin,
-                                               float tmax)
-{
-    const float4* q  = sc.pairs + 4 * (size_t)ref;
-    const float4  a  = q[0], b = q[1], c = q[2], d = q[3];
-    const uint32_t r0 = __float_as_uint(d.x), r1 = __float_as_uint(d.y), ax = __float_as_uint(d.z);
-    float         t0a = 0.0f, t0b = 0.0f;
-    const bool    ha = r0 != PNONE && pair_box(a.x, a.y, a.z, a.w, b.x, b.y, ray, inv, tmin, tmax, t0a);
-    const bool    hb = r1 != PNONE && pair_box(b.z, b.w, c.x, c.y, c.z, c.w, ray, inv, tmin, tmax, t0b);
-    PairHits      h;
-    h.n        = (int)ha + (int)hb;
-    h.near_ref = ha ? r0 : r1;
-    h.far_ref  = r1;
-    h.far_t0   = t0b;
-    if (ha && hb && near_is_second(ax << AXIS_SHIFT, ray.d)) {
-        h.near_ref = r1;
-        h.far_ref  = r0;
-        h.far_t0   = t0a;
-    }
-    return h;
-}
-
-__device__ __forceinline__ void pair_closest(const Scene& sc, const Ray& ray, float tmin, Hit& h, Stack st)
-{
-    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp  = 0;
-    uint32_t ref = 0;
-    while (true) {
-        if (!(ref & PLEAF)) {
-            const PairHits ph = pair_visit(sc, ref, ray, inv, tmin, h.t);
-            if (ph.n == 2) {
-                st.s[sp * 64 + st.lane]              = ph.far_ref;
-                st.s[(sp + st.depth) * 64 + st.lane] = __float_as_uint(ph.far_t0);
-                ++sp;
-            }
-            if (ph.n > 0) {
-                ref = ph.near_ref;
-                continue;
-            }
-        } else {
-            const uint32_t first = ref & 0x0fffffffu, cnt = (ref >> 28) & 7u;
-            for (uint32_t k = 0; k < cnt; ++k) prim_closest(sc, first + k, ray, tmin, h);
-        }
-        bool more = false;
-        while (sp > 0) {
-            --sp;
-            const float t0 = __uint_as_float(st.s[(sp + st.depth) * 64 + st.lane]);
-            if (!(t0 > h.t)) {
-                ref  = st.s[sp * 64 + st.lane];
-                more = true;
-                break;
-            }
-        }
-        if (!more) break;
-    }
-}
-
-__device__ __forceinline__ bool pair_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
-{
-    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp  = 0;
-    uint32_t ref = 0;
-    while (true) {
-        if (!(ref & PLEAF)) {
-            const PairHits ph = pair_visit(sc, ref, ray, inv, tmin, tmax);
-            if (ph.n == 2) {
-                st.s[sp * 64 + st.lane] = ph.far_ref;
-                ++sp;
-            }
-            if (ph.n > 0) {
-                ref = ph.near_ref;
-                continue;
-            }
-        } else {
-            const uint32_t first = ref & 0x0fffffffu, cnt = (ref >> 28) & 7u;
-            for (uint32_t k = 0; k < cnt; ++k)
-                if (prim_any(sc, first + k, ray, tmin, tmax)) return true;
-        }
-        if (sp == 0) break;
-        --sp;
-        ref = st.s[sp * 64 + st.lane];
-    }
-    return false;
-}
-
-
 // ------------------------------------------------------------------------------ 8-wide BVH
 // One 80-byte fetch (5 x dwordx4) tests the boxes of up to 8 children, so a ray's chain of
 // dependent node fetches is about a third of the binary walk's.  Child boxes decode to
@@ -519,7 +475,7 @@ __device__ __forceinline__ bool pair_any(const Scene& sc, const Ray& ray, float 
 __device__ __forceinline__ bool wbox(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r, const f3& inv,
                                      float tmin, float tmax, float& t0_out)
 {
-    return pair_box(lx, ly, lz, hx, hy, hz, r, inv, tmin, tmax, t0_out);
+    return slab_box(lx, ly, lz, hx, hy, hz, r, inv, tmin, tmax, t0_out);
 }
 __device__ __forceinline__ float ubyte(uint32_t w, int k) { return (float)((w >> (8 * (k & 3))) & 0xffu); }
 
@@ -567,42 +523,6 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
     return r;
 }
 
-// Closest hit: the nearest internal child is visited next; the node is pushed with the mask
-// of its other hit internal children, and on pop it is visited again restricted to that mask --
-// the boxes are re-tested against the current t_max (culling) and the nearest survivor chosen,
-// so children are taken near-first with one stack entry per level (node << 8 | mask).
-__device__ __forceinline__ void wide_closest(const Scene& sc, const Ray& ray, float tmin, Hit& h, Stack st)
-{
-    const f3 inv    = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp     = 0;
-    uint32_t node   = 0;
-    uint32_t filter = 0xffu; // first visit: every child; revisit: pending internal children only
-    while (true) {
-        const WideHits wh = wide_visit(sc, node, ray, inv, tmin, h.t, filter);
-        for (uint32_t m = wh.leaf; m; m &= m - 1) {
-            const int      k    = __ffs(m) - 1;
-            const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
-            const uint32_t base = wh.leaf_base + (meta & 31u);
-            for (uint32_t j = 0; j < (meta >> 5); ++j) prim_closest(sc, base + j, ray, tmin, h, sc.wslot_tri);
-        }
-        if (wh.inner) {
-            const uint32_t rest = wh.inner & ~(1u << wh.nearest);
-            if (rest) {
-                st.s[sp * 64 + st.lane] = (node << 8) | rest;
-                ++sp;
-            }
-            node   = wh.child_base + (uint32_t)wh.nearest;
-            filter = 0xffu;
-            continue;
-        }
-        if (sp == 0) break;
-        --sp;
-        const uint32_t e = st.s[sp * 64 + st.lane];
-        node             = e >> 8;
-        filter           = e & 0xffu;
-    }
-}
-
 __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     const f3 inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
@@ -634,90 +554,6 @@ __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float 
         if (m) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | m;
         else --sp;
         node = (e >> 8) + (uint32_t)k;
-    }
-    return false;
-}
-
-// ------------------------------------------------------------------------------ quantised BVH
-// 16-byte nodes: one dwordx4 fetch per visited node instead of two.  Boxes decode to a
-// superset of the exact boxes (outward rounding at build time), so the walk may visit a few
-// more nodes but never misses one; like near-first order this can only change which of two
-// primitives at exactly equal distance wins, so the reference-order BVH never uses it.
-__device__ __forceinline__ bool qbox_hit(const Scene& sc, const uint4& q, const Ray& r, const f3& inv, float tmin,
-                                         float tmax)
-{
-    Node n;
-    n.lo[0] = fma_f((float)(q.x & 0xffffu), sc.qscale[0], sc.qorigin[0]);
-    n.lo[1] = fma_f((float)(q.x >> 16), sc.qscale[1], sc.qorigin[1]);
-    n.lo[2] = fma_f((float)(q.y & 0xffffu), sc.qscale[2], sc.qorigin[2]);
-    n.hi[0] = fma_f((float)(q.y >> 16), sc.qscale[0], sc.qorigin[0]);
-    n.hi[1] = fma_f((float)(q.z & 0xffffu), sc.qscale[1], sc.qorigin[1]);
-    n.hi[2] = fma_f((float)(q.z >> 16), sc.qscale[2], sc.qorigin[2]);
-    return box_hit(n, r, inv, tmin, tmax);
-}
-__device__ __forceinline__ bool q_near_is_second(uint32_t meta, const f3& d)
-{
-    const uint32_t ax = (meta >> 29) & 3u;
-    const float    da = (ax == 0) ? d.x : ((ax == 1) ? d.y : d.z);
-    return da < 0.0f;
-}
-
-__device__ __forceinline__ void qnode_closest(const Scene& sc, const Ray& ray, float tmin, Hit& h, Stack st)
-{
-    const f3 inv      = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp       = 0;
-    uint32_t cur      = 0; // root: no box test
-    bool     test_box = false;
-    while (true) {
-        const uint4 q = sc.qnodes[cur];
-        if (!test_box || qbox_hit(sc, q, ray, inv, tmin, h.t)) {
-            if (q.w & QLEAF) {
-                const uint32_t first = q.w & 0x0fffffffu, cnt = (q.w >> 28) & 7u;
-                for (uint32_t k = 0; k < cnt; ++k) prim_closest(sc, first + k, ray, tmin, h);
-            } else {
-                const uint32_t c0 = q.w & 0x1fffffffu;
-                const bool     sw = q_near_is_second(q.w, ray.d);
-                st.s[sp * 64 + st.lane] = sw ? c0 : c0 + 1;
-                ++sp;
-                cur      = sw ? c0 + 1 : c0;
-                test_box = true;
-                continue;
-            }
-        }
-        if (sp == 0) break;
-        --sp;
-        cur      = st.s[sp * 64 + st.lane];
-        test_box = true;
-    }
-}
-
-__device__ __forceinline__ bool qnode_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
-{
-    const f3 inv      = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp       = 0;
-    uint32_t cur      = 0;
-    bool     test_box = false;
-    while (true) {
-        const uint4 q = sc.qnodes[cur];
-        if (!test_box || qbox_hit(sc, q, ray, inv, tmin, tmax)) {
-            if (q.w & QLEAF) {
-                const uint32_t first = q.w & 0x0fffffffu, cnt = (q.w >> 28) & 7u;
-                for (uint32_t k = 0; k < cnt; ++k)
-                    if (prim_any(sc, first + k, ray, tmin, tmax)) return true;
-            } else {
-                const uint32_t c0 = q.w & 0x1fffffffu;
-                const bool     sw = q_near_is_second(q.w, ray.d);
-                st.s[sp * 64 + st.lane] = sw ? c0 : c0 + 1;
-                ++sp;
-                cur      = sw ? c0 + 1 : c0;
-                test_box = true;
-                continue;
-            }
-        }
-        if (sp == 0) break;
-        --sp;
-        cur      = st.s[sp * 64 + st.lane];
-        test_box = true;
     }
     return false;
 }
@@ -786,7 +622,6 @@ __device__ __forceinline__ Light uload_light(const Light* p)
 }
 
 // Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
-template <bool ALLOW_WIDE = true>
 __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     Hit h;
@@ -800,20 +635,8 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
         if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
     if (sc.n_nodes == 0) return h;
-    if (ALLOW_WIDE && sc.wide_closest) {
-        wide_closest(sc, ray, tmin, h, st);
-        return h;
-    }
-    if (sc.qnodes) {
-        qnode_closest(sc, ray, tmin, h, st);
-        return h;
-    }
-    if (sc.pairs) {
-        pair_closest(sc, ray, tmin, h, st);
-        return h;
-    }
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp  = 0;
+    BinWalk  w   = bin_walk(st, sc.nodes, sc.parents, sc.stackless, sc.ordered);
     uint32_t cur = 0;      // root: no box test
     bool     test_box = false;
     while (true) {
@@ -823,18 +646,15 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
                 const uint32_t cnt = n.b & ~LEAF_BIT;
                 for (uint32_t k = 0; k < cnt; ++k) prim_closest(sc, n.a + k, ray, tmin, h);
             } else {
-                uint32_t first = n.a & CHILD_MASK, second = n.b; // reference: child 0 first
-                if (sc.ordered && near_is_second(n.a, ray.d)) { const uint32_t t = first; first = second; second = t; }
-                st.s[sp * 64 + st.lane] = second; // deferred, box tested when popped
-                ++sp;
+                uint32_t first, second; // reference: child 0 first
+                children_in_order(w, n, ray.d, first, second);
+                walk_defer(w, second); // box tested when the walk comes back to it
                 cur      = first;
                 test_box = true;
                 continue;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        cur      = st.s[sp * 64 + st.lane];
+        if (!walk_next(w, ray.d, cur)) break;
         test_box = true;
     }
     return h;
@@ -850,10 +670,8 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
     }
     if (sc.n_nodes == 0) return false;
     if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
-    if (sc.qnodes) return qnode_any(sc, ray, tmin, tmax, st);
-    if (sc.pairs) return pair_any(sc, ray, tmin, tmax, st);
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp  = 0;
+    BinWalk  w   = bin_walk(st, sc.nodes, sc.parents, sc.stackless, sc.ordered);
     uint32_t cur = 0;
     bool     test_box = false;
     while (true) {
@@ -864,18 +682,15 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
                 for (uint32_t k = 0; k < cnt; ++k)
                     if (prim_any(sc, n.a + k, ray, tmin, tmax)) return true;
             } else {
-                uint32_t first = n.a & CHILD_MASK, second = n.b;
-                if (sc.ordered && near_is_second(n.a, ray.d)) { const uint32_t t = first; first = second; second = t; }
-                st.s[sp * 64 + st.lane] = second;
-                ++sp;
+                uint32_t first, second;
+                children_in_order(w, n, ray.d, first, second);
+                walk_defer(w, second);
                 cur      = first;
                 test_box = true;
                 continue;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        cur      = st.s[sp * 64 + st.lane];
+        if (!walk_next(w, ray.d, cur)) break;
         test_box = true;
     }
     return false;
@@ -1057,7 +872,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
         return lh;
     }
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp  = 0;
+    BinWalk  w   = bin_walk(st, sc.light_nodes, sc.light_parents, sc.stackless, false);
     uint32_t cur = 0;
     bool     test_box = false;
     while (true) {
@@ -1076,16 +891,13 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
                     }
                 }
             } else {
-                st.s[sp * 64 + st.lane] = n.b;
-                ++sp;
+                walk_defer(w, n.b);
                 cur      = n.a & CHILD_MASK;
                 test_box = true;
                 continue;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        cur      = st.s[sp * 64 + st.lane];
+        if (!walk_next(w, ray.d, cur)) break;
         test_box = true;
     }
     return lh;
@@ -1110,7 +922,7 @@ __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, floa
         return false;
     }
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp  = 0;
+    BinWalk  w   = bin_walk(st, sc.light_nodes, sc.light_parents, sc.stackless, false);
     uint32_t cur = 0;
     bool     test_box = false;
     while (true) {
@@ -1124,16 +936,13 @@ __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, floa
                     if (sphere_t(l.w2o, ray, tmin, tmax, t)) return true;
                 }
             } else {
-                st.s[sp * 64 + st.lane] = n.b;
-                ++sp;
+                walk_defer(w, n.b);
                 cur      = n.a & CHILD_MASK;
                 test_box = true;
                 continue;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        cur      = st.s[sp * 64 + st.lane];
+        if (!walk_next(w, ray.d, cur)) break;
         test_box = true;
     }
     return false;

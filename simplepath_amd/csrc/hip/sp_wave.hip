@@ -29,7 +29,7 @@
 // RNG draw-ahead window (sp_path.hpp Rng): off in the wavefront kernels, where it measured
 // 1-2 % slower (it pays off in the megakernel, 2 words ahead).
 #define SP_RNG_PF 0
-#include "sp_packet.hpp"
+#include "sp_path.hpp"
 #include "sp_wave.hpp"
 
 #include <cstdlib>
@@ -157,9 +157,6 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_init(Scene sc, WaveArgs w)
 }
 
 // Primary query: Integrator::integrate's intersect_lights + intersect (Integrator.cpp:277-283).
-// WIDE: closest hit on the 8-wide BVH (SP_WIDE_CLOSEST=1); the binary instantiation carries no
-// wide-walk code, so its register count (and occupancy) stays that of the binary walk.
-template <bool WIDE>
 __global__ void __launch_bounds__(WF_BLOCK, WF_PRIM_WAVES) wf_primary(Scene sc, WaveArgs w, uint32_t sample)
 {
     extern __shared__ uint32_t lds[];
@@ -171,42 +168,30 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_PRIM_WAVES) wf_primary(Scene sc, 
     }
     if (p >= w.pe) return;
     const uint64_t t0 = w.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint32_t       steps = 0;
     const PixelRef pr = pixel_of(sc, w, p);
     float4         hrec = make_float4(0.0f, __uint_as_float(0xffffffffu), 0.0f, 0.0f);
     uint32_t       rays = 0, hits = 0;
-    const bool     on   = pr.inside && sc.max_depth > 0;
-    if (sc.packet || on) {
-        const Rsq q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
-        const Ray ray  = camera_ray(sc, pr, sample, q);
-        float     tmax = k_infinite;
-        LightHit  lh;
-        Hit       h;
-        if (sc.packet) { // whole wave together: camera rays of one tile are coherent
-            lh = scene_intersect_lights_w(sc, ray, k_ray_epsilon, tmax, on);
-            if (lh.hit) tmax = lh.t;
-            h = scene_intersect_w(sc, ray, k_ray_epsilon, tmax, on, w.diag ? &steps : nullptr);
-        } else {
-            const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
-            lh = scene_intersect_lights(sc, ray, k_ray_epsilon, tmax, st);
-            if (lh.hit) tmax = lh.t;
-            h = scene_intersect<WIDE>(sc, ray, k_ray_epsilon, tmax, st);
-        }
-        if (on) {
-            rays = 1;
-            if (h.code != 0xffffffffu) {
-                hrec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
-                hits = 1;
-            } else if (lh.hit) {
-                const rgb L = cadd(mkc(0, 0, 0), cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, q)));
-                w.acc[p]           = w.acc[p] + L.r;
-                w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
-                w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
-            }
+    if (pr.inside && sc.max_depth > 0) {
+        const Rsq   q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+        const Ray   ray  = camera_ray(sc, pr, sample, q);
+        float       tmax = k_infinite;
+        const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
+        const LightHit lh = scene_intersect_lights(sc, ray, k_ray_epsilon, tmax, st);
+        if (lh.hit) tmax = lh.t;
+        const Hit h = scene_intersect(sc, ray, k_ray_epsilon, tmax, st);
+        rays        = 1;
+        if (h.code != 0xffffffffu) {
+            hrec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
+            hits = 1;
+        } else if (lh.hit) {
+            const rgb L = cadd(mkc(0, 0, 0), cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, q)));
+            w.acc[p]           = w.acc[p] + L.r;
+            w.acc[w.n + p]     = w.acc[w.n + p] + L.g;
+            w.acc[2 * w.n + p] = w.acc[2 * w.n + p] + L.b;
         }
     }
     w.hit[p] = hrec;
-    if (w.diag) diag_record(w.diag + (size_t)(p >> 6) * 4, t0, steps, (uint32_t)__popcll(__ballot(pr.inside)));
+    if (w.diag) diag_record(w.diag + (size_t)(p >> 6) * 4, t0, 0, (uint32_t)__popcll(__ballot(pr.inside)));
     unsigned long long* slot = w.wstat + (size_t)(p >> 6) * ST_N;
     wave_count(slot, ST_RAYS, rays);
     wave_count(slot, ST_HITS, hits);
@@ -307,8 +292,10 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
     wave_count(w.wstat + (size_t)(p >> 6) * ST_N, ST_DRAWS, draws);
 }
 
-// Shadow queries, one queued ray per lane (static assignment; SP_SHADOW_DYN=0): direct_nee's
-// occlusion test (Integrator.cpp:297) -> vis[light][pixel].
+// Shadow queries, one queued ray per lane: direct_nee's occlusion test (Integrator.cpp:297) ->
+// vis[light][pixel].  (Persistent lanes that refill from the queue as their ray ends measured 2x
+// slower: refilled lanes sit at different depths of the tree and their node fetches stop
+// coalescing -- DESIGN.md §4.)
 __global__ void __launch_bounds__(WF_BLOCK, WF_TRAV_WAVES) wf_shadow(Scene sc, WaveArgs w)
 {
     extern __shared__ uint32_t lds[];
@@ -324,7 +311,6 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRAV_WAVES) wf_shadow(Scene sc, W
     const size_t   cap    = w.qcap;
     uint32_t       shadow = 0;
     const uint64_t t0     = w.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint32_t       steps  = 0;
     const uint32_t wave_g = (blockIdx.x * WF_BLOCK + threadIdx.x) >> 6;
     for (uint32_t v = wave_g; v < n_virt; v += gridDim.x * (WF_BLOCK / 64)) {
         const uint32_t j    = v % QSEG;
@@ -344,139 +330,16 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRAV_WAVES) wf_shadow(Scene sc, W
         Ray r;
         r.o = mk(o.x, o.y, o.z);
         r.d = mk(d.x, d.y, d.z);
-        bool occ;
-        if (sc.packet) {
-            occ = scene_any_w(sc, r, d.w, c.w, live, w.diag ? &steps : nullptr);
-        } else {
-            occ = live ? scene_any(sc, r, d.w, c.w, st) : true;
-        }
+        const bool occ = live ? scene_any(sc, r, d.w, c.w, st) : true;
         if (live) {
             ++shadow;
             w.vis[(size_t)li * w.n + p] = occ ? 0 : 1;
         }
     }
     if (w.diag)
-        diag_record(w.diag + ((size_t)(w.n >> 6) + (w.pb >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * 4, t0, steps,
+        diag_record(w.diag + ((size_t)(w.n >> 6) + (w.pb >> 6) + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * 4, t0, 0,
                     (uint32_t)__popcll(__ballot(shadow != 0)));
     unsigned long long* slot = w.wstat + ((size_t)w.sh_slot0 + (blockIdx.x * WF_BLOCK + threadIdx.x) / 64) * ST_N;
-    wave_count(slot, ST_RAYS, shadow); // occluded() counts the query as a ray too
-    wave_count(slot, ST_SHADOW, shadow);
-}
-
-// Shadow queries with dynamic ray fetch: persistent waves whose lanes each trace one queued
-// shadow ray (Scene::intersect_p, Scene.h:79) and take a new one as soon as theirs finishes.
-// The rays of a 64-ray batch differ in length by 10x and more (unoccluded rays cross the scene,
-// occluded ones stop at the first hit), so a wave that waited for its slowest ray left ~75 % of
-// its lanes idle (profiles/r01: lane utilisation 0.25).  Refills take a batch of items from one
-// queue segment with one atomic per wave; a wave drains its own segment, then moves on.
-// Result: vis[light][pixel] = 1 when the ray reaches the light (order-free: wf_accum sums in
-// light order).  Opt-in (SP_SHADOW_DYN=1): on the bunny frame it is 2x SLOWER than the static
-// assignment -- refilled lanes sit at different depths of the tree, so the node fetches of a
-// wave stop coalescing, and the vector L1 is what bounds traversal.
-constexpr uint32_t SHADOW_REFILL = 16; // refill when at least this many lanes are idle
-
-__global__ void __launch_bounds__(WF_BLOCK) wf_shadow_dyn(Scene sc, WaveArgs w)
-{
-    extern __shared__ uint32_t lds[];
-    const int      lane   = threadIdx.x & 63;
-    const Stack    st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
-    const uint32_t wave_g = (blockIdx.x * WF_BLOCK + threadIdx.x) >> 6;
-    uint32_t       seg    = wave_g % QSEG;
-    int            left   = QSEG; // segments not yet found empty by this wave
-    bool           busy   = false;
-    uint32_t       item = 0, cur = 0;
-    int            sp = 0;
-    bool           test_box = false;
-    Ray            r;
-    f3             inv  = mk(0, 0, 0);
-    float          tmin = 0.0f, tmax = 0.0f;
-    uint32_t       shadow = 0;
-    const uint64_t lt     = (1ull << lane) - 1ull;
-    while (true) {
-        const uint64_t idle = __ballot(!busy);
-        if (left > 0 && (uint32_t)__popcll(idle) >= SHADOW_REFILL) {
-            const uint32_t want = (uint32_t)__popcll(idle);
-            uint32_t       base = 0, got = 0;
-            while (left > 0) {
-                const uint32_t segn = w.qcount[seg * QSTRIDE];
-                uint32_t       b    = 0;
-                if (lane == 0) b = atomicAdd(w.qcount + seg * QSTRIDE + QFETCH, want);
-                b = __shfl(b, 0, 64);
-                if (b < segn) {
-                    base = b;
-                    got  = min(want, segn - b);
-                    break;
-                }
-                seg = (seg + 1) % QSEG;
-                --left;
-            }
-            const uint32_t rank = (uint32_t)__popcll(idle & lt);
-            if (!busy && rank < got) {
-                item              = w.queue[(size_t)seg * w.qcap + base + rank];
-                const int64_t  p  = item >> 5;
-                const uint32_t li = item & 31u;
-                const float4   o  = w.shp[p];
-                const float4*  e  = w.sh + ((size_t)li * w.n + p) * 2;
-                const float4   d  = e[0];
-                const float4   c  = e[1];
-                r.o  = mk(o.x, o.y, o.z);
-                r.d  = mk(d.x, d.y, d.z);
-                tmin = d.w;
-                tmax = c.w;
-                ++shadow;
-                // unbounded geometry and the lights first (any order gives the same answer)
-                bool occ = false;
-                for (int i = 0; i < sc.n_unbounded && !occ; ++i) {
-                    const UShape u = uload_shape(sc.shapes + uload_u32(sc.unbounded + i));
-                    float        t;
-                    occ = (u.kind == SP_PRIM_SPHERE) ? sphere_t(u.w2o, r, tmin, tmax, t) : plane_t(u.w2o, r, tmin, tmax, t);
-                }
-                if (!occ) occ = lights_any(sc, r, tmin, tmax, st);
-                if (occ || sc.n_nodes == 0) {
-                    w.vis[(size_t)li * w.n + p] = occ ? 0 : 1;
-                } else {
-                    busy     = true;
-                    inv      = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-                    cur      = 0; // root: no box test
-                    sp       = 0;
-                    test_box = false;
-                }
-            }
-        }
-        if (__ballot(busy) == 0) {
-            if (left == 0) break;
-            continue;
-        }
-        if (busy) { // one node of BVHAccelerator::intersect_p (BVHAccelerator.h:62-77)
-            const Node n    = sc.nodes[cur];
-            bool       next = false, occ = false;
-            if (!test_box || box_hit(n, r, inv, tmin, tmax)) {
-                if (n.b & LEAF_BIT) {
-                    const uint32_t cnt = n.b & ~LEAF_BIT;
-                    for (uint32_t k = 0; k < cnt && !occ; ++k) occ = prim_any(sc, n.a + k, r, tmin, tmax);
-                } else {
-                    uint32_t first = n.a & CHILD_MASK, second = n.b;
-                    if (sc.ordered && near_is_second(n.a, r.d)) { const uint32_t t = first; first = second; second = t; }
-                    st.s[sp * 64 + st.lane] = second;
-                    ++sp;
-                    cur      = first;
-                    test_box = true;
-                    next     = true;
-                }
-            }
-            if (!next) {
-                if (occ || sp == 0) {
-                    w.vis[(size_t)(item & 31u) * w.n + (item >> 5)] = occ ? 0 : 1;
-                    busy = false;
-                } else {
-                    --sp;
-                    cur      = st.s[sp * 64 + st.lane];
-                    test_box = true;
-                }
-            }
-        }
-    }
-    unsigned long long* slot = w.wstat + ((size_t)w.sh_slot0 + wave_g) * ST_N;
     wave_count(slot, ST_RAYS, shadow); // occluded() counts the query as a ray too
     wave_count(slot, ST_SHADOW, shadow);
 }
@@ -543,11 +406,6 @@ static int shade_waves_env()
     const char* v = std::getenv("SP_SHADE_WAVES");
     return v ? std::atoi(v) : 4;
 }
-static bool shadow_dyn_env()
-{
-    const char* v = std::getenv("SP_SHADOW_DYN"); // opt-in: slower on coherent shadow rays
-    return v ? std::atoi(v) != 0 : false;
-}
 static int32_t interleave_block_env()
 {
     const char* v = std::getenv("SP_WAVE_ILV");
@@ -582,7 +440,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     auto mark = [&]() {
         if (ev) (void)hipEventRecord(ev[e++], stream);
     };
-    const size_t stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
+    const size_t stack_lds = (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
     const size_t rs_lds    = (size_t)(2 << sc.rsqrt_bits) * 4;
     const unsigned grid_all = (unsigned)((w.n + WF_BLOCK - 1) / WF_BLOCK);
 
@@ -618,7 +476,6 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         (void)hipStreamWaitEvent(aux, fork, 0);
     }
     const uint32_t diag_sample = diag_sample_env();
-    const bool     dyn         = shadow_dyn_env();
     // waves per SIMD requested for the shading kernel (register budget vs spills)
     void (*shade)(Scene, WaveArgs, uint32_t) = wf_shade<4>;
     switch (shade_waves_env()) {
@@ -650,8 +507,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
             const WaveArgs& wi = (pw[k].diag && i == diag_sample) ? pw[k] : pd[k];
 #endif
             hipStream_t     st = ps[k];
-            if (sc.wide_closest) hipLaunchKernelGGL(wf_primary<true>, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
-            else hipLaunchKernelGGL(wf_primary<false>, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
+            hipLaunchKernelGGL(wf_primary, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
             if (k == 0) mark();
             if (parts > 1 && (k == 1 || i > 0)) (void)hipStreamWaitEvent(st, shade_done[1 - k], 0);
 #ifdef SP_SHADE_PROF
@@ -661,8 +517,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
 #endif
             if (parts > 1) (void)hipEventRecord(shade_done[k], st);
             if (k == 0) mark();
-            if (dyn) hipLaunchKernelGGL(wf_shadow_dyn, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
-            else hipLaunchKernelGGL(wf_shadow, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
+            hipLaunchKernelGGL(wf_shadow, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
             hipLaunchKernelGGL(wf_accum, dim3(grid[k]), dim3(WF_BLOCK), 0, st, sc, wi);
             if (k == 0) mark();
         }
@@ -680,7 +535,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
 
 int wave_traverse_blocks_per_cu(const Scene& sc)
 {
-    const size_t stack_lds = sc.packet ? 0 : (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
+    const size_t stack_lds = (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
     int          n         = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shadow, WF_BLOCK, stack_lds) != hipSuccess) return 1;
     return n > 0 ? n : 1;

@@ -564,18 +564,24 @@ std::string resolve(const std::string& base_dir, const std::string& p)
     return p;
 }
 
-// file_to_string (base/FileParser.cpp:821): strip blank/comment lines and trailing comments
-std::string clean_text(const std::string& text)
+// file_to_string (base/FileParser.cpp:821): strip blank/comment lines and trailing comments;
+// `lines` gets the 1-based source line of every kept character (the reference's line_numbers,
+// which its ParsingException messages quote as " on line N")
+std::string clean_text(const std::string& text, std::vector<int>& lines)
 {
     std::string        out;
     std::istringstream in(text);
+    int                line_no = 0;
+    lines.clear();
     for (std::string line; std::getline(in, line);) {
+        ++line_no;
         std::string t = trim_ws(line);
         if (t.empty() || t[0] == '#') continue;
         const size_t h = t.find('#');
         if (h != std::string::npos) t = t.substr(0, h);
         out += t;
         out.push_back(' ');
+        lines.insert(lines.end(), t.size() + 1, line_no);
     }
     return out;
 }
@@ -586,7 +592,7 @@ public:
 
     std::unique_ptr<Scene> parse(const std::string& text)
     {
-        const std::string clean = clean_text(text);
+        const std::string clean = clean_text(text, m_lines);
         Cursor            c(clean);
         if (c.token() != "version") parse_error("Expects version as first directive");
         if (c.get_char() != ':') parse_error("Expected ':' character");
@@ -601,7 +607,7 @@ public:
                                                      "sphere", "sphere_light" };
         // first pass: validate types
         collect(clean, post_version, [&](const std::string& w, const std::string&) {
-            if (!valid.count(w)) parse_error("Unknown type '" + w + "'");
+            if (!valid.count(w)) parse_error(on_line("Unknown type '" + w + "'", m_body_off));
         });
         run_pass(clean, post_version, { "scene_parameters" });
         run_pass(clean, post_version, { "environment_light", "material_glossy", "material_lambertian",
@@ -622,9 +628,11 @@ private:
             const std::string w = c.token();
             c.skip_ws();
             if (c.eof()) break;
-            if (c.get_char() != '{') parse_error("Expected '{' character");
+            const size_t at = c.pos;
+            if (c.get_char() != '{') parse_error(on_line("Expected '{' character", at));
             const size_t close = clean.find('}', c.pos);
             const std::string body = clean.substr(c.pos, close == std::string::npos ? std::string::npos : close - c.pos);
+            m_body_off = c.pos;
             c.pos = (close == std::string::npos) ? clean.size() : close + 1;
             fn(w, body);
         }
@@ -650,13 +658,14 @@ private:
     template <typename F>
     void attributes(const std::string& body, const char* what, F fn)
     {
-        Cursor c(body);
+        const size_t body_off = m_body_off;
+        Cursor       c(body);
         while (true) {
             const std::string w = c.token();
             c.skip_ws();
             if (c.eof() || c.fail) break;
-            if (c.get_char() != ':') parse_error("Expected ':' character");
-            if (!fn(w, c)) parse_error(std::string("Unknown ") + what + " attribute: " + w);
+            if (c.get_char() != ':') parse_error(on_line("Expected ':' character", body_off + c.pos));
+            if (!fn(w, c)) parse_error(on_line(std::string("Unknown ") + what + " attribute: " + w, body_off + c.pos));
             if (c.fail) break; // a failed extraction stops the reference's loop as well
         }
     }
@@ -909,8 +918,18 @@ private:
     static void to_desc(const aff& a, sp_affine& d) { put3(d.vx, a.vx); put3(d.vy, a.vy); put3(d.vz, a.vz); put3(d.p, a.p); }
     static void to_desc(const lin& a, sp_linear& d) { put3(d.vx, a.vx); put3(d.vy, a.vy); put3(d.vz, a.vz); }
 
+    // ParsingException(what, line) (base/FileParser.cpp:35): "<what> on line <N>", N = the source
+    // line of the cleaned-text offset the reference's stream had reached
+    std::string on_line(const std::string& what, size_t off) const
+    {
+        if (m_lines.empty()) return what;
+        return what + " on line " + std::to_string(m_lines[std::min(off, m_lines.size() - 1)]);
+    }
+
     std::string            m_base;
     std::unique_ptr<Scene> m_scene;
+    std::vector<int>       m_lines;        // clean_text line numbers
+    size_t                 m_body_off = 0; // clean-text offset of the block body being parsed
 };
 } // namespace
 

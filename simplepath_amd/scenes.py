@@ -631,3 +631,84 @@ def write_closed_room_scene(directory: str, max_depth: int = 40, name: str = "cl
     with open(path, "w") as fh:
         fh.write(closed_room_sp(max_depth))
     return path
+
+
+# ---------------------------------------------------------------- degenerate BVH (stackless walk)
+def wedge_strip_mesh(ratio: float = 1.9, lo_exp: int = -80, hi_exp: int = 135):
+    """A strip of wedge triangles whose sizes form a geometric series, x_i = ratio^i from about
+    6e-23 to 5e37: triangle i spans x in [x_i, 1.25 x_i] and y in [-x_i / 2, x_i / 2] on the
+    z = 0 plane (smaller ones would have a zero cross product in float and be dropped as
+    degenerate by the loader).  The reference's median split (shapes/BVHAccelerator.h:173:
+    midpoint of the bounds on the longest axis) peels only the largest triangle off at almost
+    every level, so its recursion nests 172 levels deep -- more than any LDS stack budget
+    (tests/test_gpu_parity.py: the device walks it without a stack)."""
+    i = np.arange(lo_exp, hi_exp + 1, dtype=np.float64)
+    x = (ratio ** i).astype(np.float32).astype(np.float64)
+    v = np.zeros((3 * x.size, 3), dtype=np.float32)
+    v[0::3, 0], v[0::3, 1] = x, -0.5 * x
+    v[1::3, 0], v[1::3, 1] = 1.25 * x, -0.5 * x
+    v[2::3, 0], v[2::3, 1] = x, 0.5 * x
+    f = np.arange(3 * x.size, dtype=np.int32).reshape(-1, 3)
+    return v, f
+
+
+def wedge_strip_sp(ply_rel: str, max_depth: int = 3) -> str:
+    """The wedge strip seen from above its origin, a lambertian plane under it, a sphere light
+    and an environment light."""
+    return f"""version: 1
+
+scene_parameters {{
+    output_file_name: "strip.pfm"
+    width: 64
+    height: 48
+    max_depth: {max_depth}
+}}
+
+perspective_camera {{
+    origin: 0.6 0.0 2.0
+    look_at: 0.6 0.0 0.0
+    fov: 50
+}}
+
+material_lambertian {{
+    name: "strip"
+    diffuse: 0.8 0.6 0.3
+}}
+
+material_glossy {{
+    name: "floor"
+    diffuse: 0.3 0.3 0.6
+    ior: 1.5
+    roughness: 0.3
+}}
+
+mesh {{
+    file: "{ply_rel}"
+    material: "strip"
+}}
+
+plane {{
+    material: "floor"
+    rotate: 1.0 0.0 0.0 90.0
+    translate: 0.0 0.0 -0.25
+}}
+
+sphere_light {{
+    translate: 0.5 0.5 1.5
+    scale: 0.2 0.2 0.2
+    radiance: 20.0 20.0 20.0
+}}
+
+environment_light {{
+    radiance: 0.2 0.2 0.3
+}}
+"""
+
+
+def write_wedge_strip_scene(directory: str, name: str = "wedge_strip.sp", max_depth: int = 3) -> str:
+    rel = os.path.join("ply_files", "wedge_strip.ply")
+    _write_once(os.path.join(directory, rel), lambda p: write_ply(p, *wedge_strip_mesh()))
+    path = os.path.join(directory, name)
+    with open(path, "w") as fh:
+        fh.write(wedge_strip_sp(rel, max_depth))
+    return path

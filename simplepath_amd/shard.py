@@ -21,16 +21,19 @@ def per_rank_capacity(n_tiles: int, world: int) -> int:
     return (n_tiles + world - 1) // world
 
 
-def gather_frame(local_tiles, n_tiles: int, rank: int, world: int, dist, gathered=None, frame=None):
+def gather_frame(local_tiles, n_tiles: int, rank: int, world: int, dist, gathered=None, frame=None,
+                 collective: bool = False):
     """Collect the tile buffers of all ranks on rank 0.
 
-    local_tiles: torch tensor [per_rank_capacity, 64, 3] holding this rank's shard in shard order.
+    local_tiles: torch tensor [per_rank_capacity, 64, 3] holding this rank's shard in shard order
+    (a CUDA tensor under the nccl = RCCL backend, a CPU tensor under gloo).
     Returns, on rank 0, `frame` [n_tiles, 64, 3] in scheduler order (allocated if not given);
     None elsewhere.  `gathered` may be a preallocated list of `world` tensors shaped like
-    local_tiles (rank 0 only)."""
+    local_tiles (rank 0 only).  With world == 1 the copy is local unless `collective` is set
+    (then the same dist.gather runs over the one-rank group: device tests of the RCCL path)."""
     import torch
 
-    if world == 1:
+    if world == 1 and not collective:
         if frame is None:
             return local_tiles[:n_tiles]
         frame.copy_(local_tiles[:n_tiles])

@@ -25,4 +25,6 @@ def scene_dir(tmp_path_factory):
     scenes.write_elf_scene(d, n=24, max_depth=16, name="elf_small.sp")
     # recursion deeper than the device's in-register levels (32)
     scenes.write_closed_room_scene(d, max_depth=40)
+    # a reference BVH 172 levels deep (geometric wedge strip): the stackless walk
+    scenes.write_wedge_strip_scene(d)
     return d

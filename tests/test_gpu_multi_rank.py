@@ -67,3 +67,43 @@ def test_two_ranks_on_device_match_single_process(scene_dir, tmp_path):
     assert st.pipeline == 2
     assert frame.shape == ref.shape
     assert np.array_equal(frame.view(np.uint32), ref.view(np.uint32))
+
+
+def _nccl_worker(rank, world, port, result_path):
+    """Renders its shard on device `rank`, gathers the CUDA tile buffers over RCCL."""
+    import datetime
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120),
+                            device_id=torch.device(f"cuda:{rank}"))
+    from simplepath_amd import shard
+
+    n = 45
+    mine = shard.shard_tiles(n, rank, world)
+    local = torch.full((shard.per_rank_capacity(n, world), 64, 3), -1.0, dtype=torch.float32, device=f"cuda:{rank}")
+    # tile t holds the value t in every lane: the assembled frame must be tile-ordered
+    local[: len(mine)] = torch.from_numpy(mine.astype(np.float32)).to(f"cuda:{rank}")[:, None, None]
+    frame = shard.gather_frame(local, n, rank, world, dist, collective=True)
+    if rank == 0:
+        assert frame.is_cuda
+        np.save(result_path, frame.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [1, 2])
+def test_rccl_gather_frame_on_device(tmp_path, world):
+    # the frame-end collective bench.py times: dist.gather of CUDA tensors over nccl (= RCCL);
+    # world 1 runs the same collective through a one-rank group, world 2 needs two GPUs
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs")
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_nccl_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    frame = np.load(out)
+    assert frame.shape == (45, 64, 3)
+    assert np.array_equal(frame, np.broadcast_to(np.arange(45, dtype=np.float32)[:, None, None], frame.shape))

@@ -301,3 +301,41 @@ def test_deep_recursion_bitexact(scene_dir, integrator):
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
     if integrator == "brute_force":
         assert gst.rays > 16 * 16 * 2 * 20  # mean path length > 20: many paths go past level 32
+
+
+@pytest.mark.parametrize("integrator,pipeline", [("direct_lighting", "megakernel"), ("direct_lighting", "wavefront"),
+                                                 ("direct_lighting", "chunks"), ("iterative_rrnee", "megakernel"),
+                                                 ("iterative_rrnee", "wavefront"), ("whitted", "megakernel")])
+def test_degenerate_deep_bvh_stackless_bitexact(scene_dir, integrator, pipeline):
+    # a reference BVH 172 levels deep (the reference's recursion is unbounded, BVHAccelerator.h:
+    # 62-77): past the LDS budget, so every walk climbs parent links instead of a stack -- same
+    # nodes, same order, same box tests: bit-exact against the oracle and the reference build
+    s = load(scene_dir, "wedge_strip.sp", 64, 48, bvh=1)
+    assert s.bvh_info()["depth"] == 172
+    g, gst = sp.render_tiles(s, integrator, 3, pipeline=pipeline)
+    assert gst.stack_depth == 0  # stackless
+    t = sp.string_to_integrator_type(integrator)
+    c, cst = _oracle.render(s, t, 3, variant="glibc")
+    assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
+    assert g.max() > 0.0
+
+
+@pytest.mark.parametrize("scene,w,h", [("bunny.sp", 64, 40), ("lucy_small.sp", 40, 56), ("material_spheres_ibl.sp", 24, 48)])
+@pytest.mark.parametrize("integrator", ["direct_lighting", "iterative_rrnee"])
+def test_forced_stackless_walk(scene_dir, monkeypatch, scene, w, h, integrator):
+    # SP_STACKLESS=1: the parent-link walk on ordinary scenes -- bit-exact vs the oracle on the
+    # reference BVH, and bit-identical to the stack walk on the SAH binary BVH (near-first order)
+    monkeypatch.setenv("SP_STACKLESS", "1")
+    s = load(scene_dir, scene, w, h, bvh=1)
+    g, gst = sp.render_tiles(s, integrator, 3)
+    assert gst.stack_depth == 0
+    c, _ = _oracle.render(s, sp.string_to_integrator_type(integrator), 3, variant="spm")
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
+    a, ast = sp.render_tiles(load(scene_dir, scene, w, h, bvh=0), integrator, 3)
+    monkeypatch.setenv("SP_STACKLESS", "0")
+    monkeypatch.setenv("SP_WIDE", "0")  # the stackless scene walks the binary SAH BVH for any-hit too
+    b, bst = sp.render_tiles(load(scene_dir, scene, w, h, bvh=0), integrator, 3)
+    assert ast.stack_depth == 0 and bst.stack_depth > 0
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
+    assert (ast.rays, ast.shadow_rays, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.rng_draws)

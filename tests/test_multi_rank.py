@@ -74,3 +74,31 @@ def test_shards_partition_the_frame():
             allt = np.sort(np.concatenate(parts))
             assert np.array_equal(allt, np.arange(n))
             assert max(len(p) for p in parts) == shard.per_rank_capacity(n, world)
+
+
+def test_bench_launcher_spawns_ranks():
+    # `python bench.py --gpus 2` without torchrun: bench.py starts the ranks itself (as child
+    # processes, before any GPU call) through torch.distributed.run on 127.0.0.1
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-selftest"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line == {"launch_selftest": True, "world": 2, "rank_sum": 1.0}
+
+
+def test_bench_launch_command():
+    sys_path = os.path.join(ROOT, "bench.py")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", sys_path)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    cmd = b.launch_command(["--gpus", "8", "--steps", "3"], 8, 29555)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]

@@ -136,3 +136,16 @@ def test_deep_recursion(ref, scene_dir, integrator):
     o = oracle_render(path, 16, 16, t, 2, ids)
     assert same(r, o), (integrator, float(np.abs(r - o).max()))
     assert r.max() > 0.0
+
+
+@pytest.mark.parametrize("integrator", ["direct_lighting", "iterative_rrnee"])
+def test_degenerate_deep_bvh(ref, scene_dir, integrator):
+    """A wedge strip whose reference BVH nests 172 levels (shapes/BVHAccelerator.h:62-77 recurses
+    without bound): the oracle's recursive walk and the reference agree bit for bit."""
+    path = os.path.join(scene_dir, "wedge_strip.sp")
+    t = sp.string_to_integrator_type(integrator)
+    ids = np.arange(sp.TileScheduler(64, 48).get_num_tiles(), dtype=np.int32)
+    r = ref_render(ref, path, 64, 48, t, 3, ids)
+    o = oracle_render(path, 64, 48, t, 3, ids)
+    assert same(r, o), (integrator, float(np.abs(r - o).max()))
+    assert r.max() > 0.0

@@ -41,6 +41,47 @@ def test_parse_errors():
     assert "already exists" in str(e.value)
 
 
+def _example_like_scene() -> str:
+    """The top-level block sequence of the reference's example_scene.sp (BASELINE configs[0]):
+    a transmissive dielectric, a lambertian, a comment, then a `material_layered` block on line 26
+    and `primitive` / `instance` blocks later on."""
+    head = ('version: 1\n\nscene_parameters {\n    output_file_name: "image.pfm"\n    width: 800\n    height: 600\n}\n\n'
+            'perspective_camera {\n    origin: 0.0 2.0 5.0\n    look_at: 0.0 1.0 0.0\n    fov: 45\n}\n\n'
+            'material_transmissive_dielectric {\n    name: "coat"\n    ior: 1.3\n}\n\n'
+            'material_lambertian {\n    name: "base"\n    diffuse: 0.1 0.2 0.8\n}\n\n'
+            '# layered materials list the topmost layer first\n')
+    assert head.count("\n") == 25
+    return head + ('material_layered {\n    name: "m0"\n    layer: "coat"\n    layer: "base"\n}\n\n'
+                   'primitive {\n    geometry: "g"\n    material: "m0"\n}\n')
+
+
+def test_example_scene_rejected_like_reference():
+    """configs[0] (example_scene.sp): the reference's first parser pass binary-searches every
+    top-level word in valid_top_level_types (base/FileParser.cpp:231-249) and throws
+    ParsingException("Unknown type 'material_layered'", line) (FileParser.cpp:866-873), whose
+    message is "<what> on line <N>" (FileParser.cpp:35-38), before any block is parsed."""
+    with pytest.raises(sp.SimplePathError) as e:
+        sp.Scene.from_string(_example_like_scene())
+    assert e.value.code == -1  # SP_ERR_PARSE
+    assert str(e.value).endswith("Unknown type 'material_layered' on line 26")
+    ref = "/root/reference/example_scene.sp"
+    if os.path.exists(ref):  # the reference's own file, where it is present (this container)
+        with pytest.raises(sp.SimplePathError) as e:
+            sp.Scene.from_file(ref)
+        assert e.value.code == -1
+        assert str(e.value).endswith("Unknown type 'material_layered' on line 26")
+
+
+def test_parse_error_line_numbers():
+    # blank and comment lines are not counted out: N is the line in the original file
+    with pytest.raises(sp.SimplePathError) as e:
+        sp.Scene.from_string("version: 1\n\n# c\nperspective_camera {\n origin: 0 0 1\n bogus: 1\n}\n")
+    assert str(e.value).endswith("Unknown perspective_camera attribute: bogus on line 6")
+    with pytest.raises(sp.SimplePathError) as e:
+        sp.Scene.from_string("version: 1\n\n\nsphere (\n}\n")
+    assert str(e.value).endswith("Expected '{' character on line 4")
+
+
 def test_set_resolution_rebuilds_camera(scene_dir):
     s = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp"))
     a = s.desc().camera.transform
@@ -120,3 +161,15 @@ def test_ascii_stl_unsupported(tmp_path):
                              'material_lambertian {\n name: "m"\n diffuse: 1 1 1\n}\n'
                              'mesh {\n file: "a.stl"\n material: "m"\n}\n', str(tmp_path))
     assert "ASCII STL" in str(e.value)
+
+
+def test_degenerate_strip_bvh_is_stackless(scene_dir):
+    # host-only BVH statistics: the reference split nests 172 levels, past the LDS budget (96),
+    # so the device walks it without a stack; SAH stays shallow and keeps its stack
+    s = sp.Scene.from_file(os.path.join(scene_dir, "wedge_strip.sp"))
+    ref = s.bvh_build_info(1)
+    sah = s.bvh_build_info(0)
+    assert ref["depth"] == 172 and ref["stack_depth"] == 0 and ref["wide_depth"] == 0
+    assert sah["depth"] < 64 and sah["stack_depth"] == max(sah["depth"], sah["wide_depth"], sah["light_depth"]) + 1
+    b = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp")).bvh_build_info(1)
+    assert b["stack_depth"] == b["depth"] + 1

@@ -2,7 +2,7 @@
 # Round bench session: GPU parity tests, the default bench line (with CPU baseline), and a
 # rocprofv3 kernel-trace summary of the same command.
 set -o pipefail
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1

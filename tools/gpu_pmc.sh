@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes (separate runs, kernel-trace only) on a reduced bench (same frame, 32 spp).
 set -o pipefail
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT

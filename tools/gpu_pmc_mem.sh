@@ -1,7 +1,7 @@
 #!/bin/bash
 # Memory-pipeline PMC passes (TA/TD/TCP) on a reduced bench; one counter set per rocprofv3 run.
 set -o pipefail
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/pmc2}
 mkdir -p $OUT
 export TMPDIR=/tmp

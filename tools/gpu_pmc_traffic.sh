@@ -2,7 +2,7 @@
 # FETCH_SIZE and WRITE_SIZE (separate passes: they cannot share one) on the default bench frame,
 # then per-launch HBM bytes per kernel -> gpurun_out/pmc_bench_bunny.json.
 set -o pipefail
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/.."
 R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out/pmct
 export TMPDIR=/tmp

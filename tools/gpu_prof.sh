@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary of one bench configuration ($BENCH_ARGS) -> gpurun_out/$NAME
 set -o pipefail
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/.."
 R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc passes (run_pmc.sh) per kernel.
+"""Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh) per kernel.
 
 Usage: python3 tools/pmc_summary.py gpurun_out/pmc [--json out.json]
 

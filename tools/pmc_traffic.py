@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""HBM traffic per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (run_pmc_traffic.sh).
+"""HBM traffic per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/gpu_pmc_traffic.sh).
 
 Correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reports half the bytes of coalesced reads on
 gfx950 -> doubled; WRITE_SIZE is exact.  Both are in KiB.  Calibrated on this code's own
