@@ -263,6 +263,17 @@ int  sp_tiles_to_image(int32_t width, int32_t height, const int32_t* tile_ids, i
 /* Write an image as PFM exactly as Image/Image.cpp:40 write_pfm does. */
 int  sp_write_pfm(const char* path, int32_t width, int32_t height, const float* image);
 
+/* RSQRTSS emulation table.  The reference normalises with RSQRTSS + one Newton step
+ * (math/Math.h:205); RSQRTSS is a hardware table whose outputs differ between CPU vendors, so the
+ * reference's images are those of the CPU it ran on.  By default scenes are built (host) and
+ * rendered (device) with the table of this host's CPU, captured at start-up.  sp_rsqrt_table_set
+ * installs another CPU's table -- e.g. the one recorded with a golden image made elsewhere -- for
+ * every scene loaded and uploaded afterwards (entries == NULL: back to this host's table).
+ * entries holds 2 << bits words: [exponent parity][leading mantissa bits]. */
+int  sp_rsqrt_table_get(uint32_t* entries, int64_t capacity, int32_t* bits, uint32_t* zero_result,
+                        uint32_t* denorm_result);
+int  sp_rsqrt_table_set(const uint32_t* entries, int32_t bits, uint32_t zero_result, uint32_t denorm_result);
+
 /* Numerics self-checks used by the tests (no GPU needed). */
 int  sp_rsqrt_table_info(int32_t* mantissa_bits, int32_t* verified);
 float sp_host_rsqrt_emulated(float x); /* table emulation of RSQRTSS, host-evaluated */

@@ -24,7 +24,7 @@ from ._abi import INTEGRATORS, SimplePathError, check, lib
 __all__ = [
     "Scene", "TileScheduler", "ColumnMajorTileScheduler", "RenderStats", "render", "render_tiles",
     "render_tiles_device", "tiles_to_image", "write_pfm", "string_to_integrator_type", "INTEGRATORS",
-    "SimplePathError", "k_tile_dimension",
+    "SimplePathError", "k_tile_dimension", "rsqrt_table", "set_rsqrt_table",
 ]
 
 k_tile_dimension = 8  # base/Tile.h:10
@@ -219,6 +219,27 @@ def tiles_to_image(width: int, height: int, tiles: np.ndarray, tile_ids: Optiona
                                   0 if ids is None else ids.size,
                                   t.ctypes.data_as(C.POINTER(C.c_float)), img.ctypes.data_as(C.POINTER(C.c_float))))
     return img
+
+
+def rsqrt_table() -> dict:
+    """The RSQRTSS table scenes are built and rendered with (sp_rsqrt_table_get)."""
+    bits, zero, den = C.c_int32(), C.c_uint32(), C.c_uint32()
+    check(lib().sp_rsqrt_table_get(None, 0, C.byref(bits), C.byref(zero), C.byref(den)))
+    entries = np.zeros(2 << bits.value, dtype=np.uint32)
+    check(lib().sp_rsqrt_table_get(entries.ctypes.data_as(C.POINTER(C.c_uint32)), entries.size, None, None, None))
+    return {"entries": entries, "bits": bits.value, "zero_result": zero.value, "denorm_result": den.value}
+
+
+def set_rsqrt_table(table: Optional[dict]) -> None:
+    """Emulate another CPU's RSQRTSS (a table from rsqrt_table() there); None: this host's."""
+    if table is None:
+        check(lib().sp_rsqrt_table_set(None, 0, 0, 0))
+        return
+    e = np.ascontiguousarray(table["entries"], dtype=np.uint32)
+    if e.size != 2 << int(table["bits"]):
+        raise ValueError("RSQRTSS table: entries must hold 2 << bits words")
+    check(lib().sp_rsqrt_table_set(e.ctypes.data_as(C.POINTER(C.c_uint32)), int(table["bits"]),
+                                   int(table["zero_result"]), int(table["denorm_result"])))
 
 
 def write_pfm(path: str, image: np.ndarray) -> None:

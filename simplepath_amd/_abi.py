@@ -130,6 +130,9 @@ SIGNATURES = {
     "sp_tiles_to_image": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int64,
                                     C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "sp_write_pfm": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_float)]),
+    "sp_rsqrt_table_get": (C.c_int, [C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint32)]),
+    "sp_rsqrt_table_set": (C.c_int, [C.POINTER(C.c_uint32), C.c_int32, C.c_uint32, C.c_uint32]),
     "sp_rsqrt_table_info": (C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "sp_host_rsqrt_emulated": (C.c_float, [C.c_float]),
 }

@@ -452,6 +452,31 @@ int sp_rsqrt_table_info(int32_t* mantissa_bits, int32_t* verified)
     return SP_OK;
 }
 
+int sp_rsqrt_table_get(uint32_t* entries, int64_t capacity, int32_t* bits, uint32_t* zero_result,
+                       uint32_t* denorm_result)
+{
+    const auto& c = sph::rsqrt_active();
+    if (c.entries.empty()) return fail(SP_ERR_UNSUPPORTED, "RSQRTSS table capture failed");
+    if (bits) *bits = c.bits;
+    if (zero_result) *zero_result = c.zero_result;
+    if (denorm_result) *denorm_result = c.denorm_result;
+    if (entries) {
+        if (capacity < (int64_t)c.entries.size()) return fail(SP_ERR_ARG, "RSQRTSS table: capacity too small");
+        std::memcpy(entries, c.entries.data(), c.entries.size() * sizeof(uint32_t));
+    }
+    return SP_OK;
+}
+
+int sp_rsqrt_table_set(const uint32_t* entries, int32_t bits, uint32_t zero_result, uint32_t denorm_result)
+{
+    try {
+        sph::rsqrt_set_override(entries, bits, zero_result, denorm_result);
+        return SP_OK;
+    } catch (const sph::SpError& e) {
+        return fail(e.code, e.what());
+    }
+}
+
 float sp_host_rsqrt_emulated(float x)
 {
     const auto&     c = sph::rsqrt_capture();
@@ -475,7 +500,7 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
     spd::Scene&       d = s->dev;
     d                   = spd::Scene{};
 
-    const auto& rc = sph::rsqrt_capture();
+    const auto& rc = sph::rsqrt_active();
     if (rc.entries.empty()) return fail(SP_ERR_UNSUPPORTED, "RSQRTSS table capture failed");
     if (!rc.verified) return fail(SP_ERR_UNSUPPORTED, "RSQRTSS table could not be verified on this host CPU");
 
@@ -751,10 +776,27 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     int64_t wave_min = 24000, chunk_max = 12000;
     if (const char* v = std::getenv("SP_WAVE_MIN_TILES")) wave_min = std::atoll(v);
     if (const char* v = std::getenv("SP_CHUNK_MAX_TILES")) chunk_max = std::atoll(v);
+    // sample-chunk buffers: per-sample hit records and radiance, the generator store (a
+    // DirectLighting sample draws at most 34 words per light: Light::sample 2 + glossy rho 32; +2
+    // generations for the first twist and the one rng_prepare may twist ahead), chunk starts
+    const uint32_t spp_u   = p->samples_per_pixel;
+    int64_t ck_chunks = 1; // chunks per pixel, then of ck_len samples each (the last may be short)
+    while (ck_chunks < 32 && n_tiles * ck_chunks < 120000) ck_chunks *= 2;
+    if (const char* v = std::getenv("SP_CHUNKS")) ck_chunks = std::max<int64_t>(1, std::atoll(v));
+    ck_chunks              = std::min<int64_t>(ck_chunks, spp_u);
+    const uint32_t ck_len  = (uint32_t)((spp_u + ck_chunks - 1) / ck_chunks);
+    ck_chunks              = (spp_u + ck_len - 1) / ck_len;
+    const uint64_t ck_max_draws = (uint64_t)spp_u * (uint64_t)std::max(1, s->dev.n_lights) * 34;
+    const uint32_t ck_gens      = (uint32_t)((ck_max_draws + spm::MT_N - 1) / spm::MT_N + 2);
+    const double   ck_base_bytes = (double)n_tiles * 64 * spp_u * (16 + 12 + 2) +
+                                 (double)n_tiles * ck_gens * spm::MT_N * 64 * 8 + (double)ck_chunks * n_tiles * 64 * 4;
+    double ck_max_gb = 96.0;
+    if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) ck_max_gb = std::atof(v);
     if (pipeline == SP_PIPELINE_AUTO) {
         if (wave_ok && n_tiles >= wave_min) pipeline = SP_PIPELINE_WAVEFRONT;
-        else if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && n_tiles < chunk_max) pipeline = SP_PIPELINE_SAMPLE_CHUNKS;
-        else pipeline = SP_PIPELINE_MEGAKERNEL;
+        else if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && n_tiles < chunk_max && ck_base_bytes <= ck_max_gb * 1e9)
+            pipeline = SP_PIPELINE_SAMPLE_CHUNKS;
+        else pipeline = SP_PIPELINE_MEGAKERNEL; // also when the chunk buffers would not fit the budget
     }
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
     int                launches = 0, parts_used = 1;
@@ -926,22 +968,14 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         const int    rs_words  = 2 << s->dev.rsqrt_bits;
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
-        const uint32_t spp    = (uint32_t)p->samples_per_pixel;
-        int64_t        chunks = 1;
-        while (chunks < 32 && n_tiles * chunks < 120000) chunks *= 2;
-        if (const char* v = std::getenv("SP_CHUNKS")) chunks = std::max<int64_t>(1, std::atoll(v));
-        chunks = std::min<int64_t>(chunks, spp);
-        const uint32_t chunk_len = (uint32_t)((spp + chunks - 1) / chunks);
-        chunks                   = (spp + chunk_len - 1) / chunk_len;
-        const size_t n_px     = (size_t)n_tiles * 64;
-        const size_t b_hits   = n_px * spp * 16;
-        const size_t b_L      = n_px * spp * 12;
-        // generator store: every generation a pixel's stream reaches; a DirectLighting sample draws
-        // at most 34 words per light (Light::sample 2 + glossy rho estimate 32), +2 generations for
-        // the first twist and the one rng_prepare may twist ahead
-        const uint64_t max_draws = (uint64_t)spp * (uint64_t)std::max(1, s->dev.n_lights) * 34;
-        const uint32_t gens      = (uint32_t)((max_draws + spm::MT_N - 1) / spm::MT_N + 2);
-        const size_t b_snap   = (size_t)n_tiles * gens * spm::MT_N * 64 * 8;
+        const uint32_t spp       = spp_u;
+        const int64_t  chunks    = ck_chunks;
+        const uint32_t chunk_len = ck_len;
+        const size_t   n_px      = (size_t)n_tiles * 64;
+        const size_t   b_hits    = n_px * spp * 16;
+        const size_t   b_L       = n_px * spp * 12;
+        const uint32_t gens      = ck_gens; // generator store: every generation a pixel's stream reaches
+        const size_t   b_snap    = (size_t)n_tiles * gens * spm::MT_N * 64 * 8;
         const size_t b_ctl    = (size_t)chunks * n_px * 4;
         // per-sample draw counts from the camera pass unless an image light makes them depend on
         // the drawn numbers (then ck_count replays Light::sample)
@@ -956,8 +990,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         size_t b_sray = n_px * spp * (size_t)std::max(1, s->dev.n_lights) * 48;
         bool   split  = false;
         if (const char* v = std::getenv("SP_CHUNK_SPLIT")) split = std::atoi(v) != 0 && s->dev.n_lights <= 8;
-        double max_gb = 96.0;
-        if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) max_gb = std::atof(v);
+        const double max_gb = ck_max_gb;
         if ((double)(b_hits + b_L + b_snap + b_ctl + b_draws + b_sray) > max_gb * 1e9) split = false;
         if (!split) b_sray = 0;
         const size_t need_b   = b_hits + b_L + b_snap + b_ctl + b_draws + b_sray + 4 * 256;

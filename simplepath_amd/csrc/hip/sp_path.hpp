@@ -370,15 +370,9 @@ struct Stack {
     int       depth; // entries; pair traversal keeps each entry's entry distance at s[(e + depth) * 64 + lane]
 };
 
-// SAH nodes carry their split axis: the child on the far side of the ray's direction goes on
-// the stack.  Only the visiting order changes (closest hit: equal-distance ties may resolve to
+// SAH nodes carry their split axis: the child on the far side of the ray's direction is
+// deferred.  Only the visiting order changes (closest hit: equal-distance ties may resolve to
 // another primitive; any hit: no change), so the reference-order BVH never uses it.
-__device__ __forceinline__ bool near_is_second(uint32_t a, const f3& d)
-{
-    const uint32_t ax = a >> AXIS_SHIFT;
-    const float    da = (ax == 0) ? d.x : ((ax == 1) ? d.y : d.z);
-    return da < 0.0f;
-}
 
 // Depth-first walk of a binary BVH in the reference's recursion order: a node's second child is
 // deferred while the first child's subtree is walked, and box-tested (against the limits current
@@ -387,35 +381,46 @@ __device__ __forceinline__ bool near_is_second(uint32_t a, const f3& d)
 // from the finished subtree to the first ancestor entered through its first child: the same
 // nodes, in the same order, with the same box tests, and no per-lane memory at all (a degenerate
 // median-split tree can nest thousands of levels, like the reference's recursion).
+// SL (stackless) is a template parameter so the stack walk compiles to exactly the loop it was.
+template <bool SL>
 struct BinWalk {
     Stack           st;
     int             sp;
     const Node*     nodes;
-    const uint32_t* parents; // non-null: stackless
+    const uint32_t* parents; // SL: parent links
     bool            ordered; // SAH near-first order
+    uint32_t        dneg;    // bit a: ray direction component a < 0 (near_is_second without selects)
 };
-__device__ __forceinline__ BinWalk bin_walk(Stack st, const Node* nodes, const uint32_t* parents, bool stackless,
-                                            bool ordered)
+__device__ __forceinline__ uint32_t dir_sign_bits(const f3& d)
 {
-    return BinWalk{ st, 0, nodes, stackless ? parents : nullptr, ordered };
+    return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
 }
-__device__ __forceinline__ void children_in_order(const BinWalk& w, const Node& n, const f3& d, uint32_t& first,
+template <bool SL>
+__device__ __forceinline__ BinWalk<SL> bin_walk(Stack st, const Node* nodes, const uint32_t* parents, bool ordered,
+                                                const f3& d)
+{
+    return BinWalk<SL>{ st, 0, nodes, parents, ordered, dir_sign_bits(d) };
+}
+template <bool SL>
+__device__ __forceinline__ void children_in_order(const BinWalk<SL>& w, const Node& n, const f3&, uint32_t& first,
                                                   uint32_t& second)
 {
     first  = n.a & CHILD_MASK;
     second = n.b;
-    if (w.ordered && near_is_second(n.a, d)) { const uint32_t t = first; first = second; second = t; }
+    if (w.ordered && ((w.dneg >> (n.a >> AXIS_SHIFT)) & 1u)) { const uint32_t t = first; first = second; second = t; }
 }
-__device__ __forceinline__ void walk_defer(BinWalk& w, uint32_t second)
+template <bool SL>
+__device__ __forceinline__ void walk_defer(BinWalk<SL>& w, uint32_t second)
 {
-    if (w.parents) return;
+    if (SL) return;
     w.st.s[w.sp * 64 + w.st.lane] = second;
     ++w.sp;
 }
 // The next deferred node after the subtree at `cur` is finished; false when the walk is done.
-__device__ __forceinline__ bool walk_next(BinWalk& w, const f3& d, uint32_t& cur)
+template <bool SL>
+__device__ __forceinline__ bool walk_next(BinWalk<SL>& w, const f3& d, uint32_t& cur)
 {
-    if (!w.parents) {
+    if (!SL) {
         if (w.sp == 0) return false;
         --w.sp;
         cur = w.st.s[w.sp * 64 + w.st.lane];
@@ -621,22 +626,12 @@ __device__ __forceinline__ Light uload_light(const Light* p)
     return l;
 }
 
-// Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
-__device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+// BVHAccelerator::intersect (shapes/BVHAccelerator.h:62-77) over the binary BVH
+template <bool SL>
+__device__ __forceinline__ Hit bvh_closest(const Scene& sc, const Ray& ray, float tmin, Hit h, Stack st)
 {
-    Hit h;
-    h.t    = tmax;
-    h.code = 0xffffffffu;
-    for (int i = 0; i < sc.n_unbounded; ++i) {
-        const int    sid = (int)uload_u32(sc.unbounded + i);
-        const UShape s   = uload_shape(sc.shapes + sid);
-        float        t;
-        const bool  hit = (s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
-        if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
-    }
-    if (sc.n_nodes == 0) return h;
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    BinWalk  w   = bin_walk(st, sc.nodes, sc.parents, sc.stackless, sc.ordered);
+    BinWalk<SL> w = bin_walk<SL>(st, sc.nodes, sc.parents, sc.ordered != 0, ray.d);
     uint32_t cur = 0;      // root: no box test
     bool     test_box = false;
     while (true) {
@@ -660,18 +655,29 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
     return h;
 }
 
-// any-hit over the geometry accelerator (ListAccelerator::intersect_p_impl)
-__device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+// Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
+__device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
+    Hit h;
+    h.t    = tmax;
+    h.code = 0xffffffffu;
     for (int i = 0; i < sc.n_unbounded; ++i) {
-        const UShape s = uload_shape(sc.shapes + uload_u32(sc.unbounded + i));
+        const int    sid = (int)uload_u32(sc.unbounded + i);
+        const UShape s   = uload_shape(sc.shapes + sid);
         float        t;
-        if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
+        const bool  hit = (s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
+        if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
-    if (sc.n_nodes == 0) return false;
-    if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
+    if (sc.n_nodes == 0) return h;
+    return sc.stackless ? bvh_closest<true>(sc, ray, tmin, h, st) : bvh_closest<false>(sc, ray, tmin, h, st);
+}
+
+// BVHAccelerator::intersect_p over the binary BVH
+template <bool SL>
+__device__ __forceinline__ bool bvh_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    BinWalk  w   = bin_walk(st, sc.nodes, sc.parents, sc.stackless, sc.ordered);
+    BinWalk<SL> w = bin_walk<SL>(st, sc.nodes, sc.parents, sc.ordered != 0, ray.d);
     uint32_t cur = 0;
     bool     test_box = false;
     while (true) {
@@ -694,6 +700,19 @@ __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, fl
         test_box = true;
     }
     return false;
+}
+
+// any-hit over the geometry accelerator (ListAccelerator::intersect_p_impl)
+__device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    for (int i = 0; i < sc.n_unbounded; ++i) {
+        const UShape s = uload_shape(sc.shapes + uload_u32(sc.unbounded + i));
+        float        t;
+        if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
+    }
+    if (sc.n_nodes == 0) return false;
+    if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
+    return sc.stackless ? bvh_any<true>(sc, ray, tmin, tmax, st) : bvh_any<false>(sc, ray, tmin, tmax, st);
 }
 
 // ------------------------------------------------------------------------------ image environment light
@@ -836,6 +855,42 @@ struct LightHit {
 // LightIntersection::L of a hit (light_hit_L evaluates an image light lazily: the integrators
 // only read L when no geometry is in front of the light).
 
+// the sphere lights' BVH (child 0 first: reference build)
+template <bool SL>
+__device__ __forceinline__ LightHit light_bvh_closest(const Scene& sc, const Ray& ray, float tmin, LightHit lh, Stack st)
+{
+    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    BinWalk<SL> w = bin_walk<SL>(st, sc.light_nodes, sc.light_parents, false, ray.d);
+    uint32_t cur = 0;
+    bool     test_box = false;
+    while (true) {
+        const Node n = sc.light_nodes[cur];
+        if (!test_box || box_hit(n, ray, inv, tmin, lh.t)) {
+            if (n.b & LEAF_BIT) {
+                const uint32_t cnt = n.b & ~LEAF_BIT;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const Light& l = sc.lights[sc.light_slot[n.a + k]];
+                    float        t;
+                    if (sphere_t(l.w2o, ray, tmin, lh.t, t)) {
+                        lh.hit = true;
+                        lh.t   = t;
+                        lh.L   = l.radiance;
+                        lh.env = -1;
+                    }
+                }
+            } else {
+                walk_defer(w, n.b);
+                cur      = n.a & CHILD_MASK;
+                test_box = true;
+                continue;
+            }
+        }
+        if (!walk_next(w, ray.d, cur)) break;
+        test_box = true;
+    }
+    return lh;
+}
+
 // Scene::intersect_lights (base/Scene.h:69): ListAccelerator{environment..., BVH(sphere lights)}
 __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
@@ -871,36 +926,7 @@ __device__ __forceinline__ LightHit scene_intersect_lights(const Scene& sc, cons
         }
         return lh;
     }
-    const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    BinWalk  w   = bin_walk(st, sc.light_nodes, sc.light_parents, sc.stackless, false);
-    uint32_t cur = 0;
-    bool     test_box = false;
-    while (true) {
-        const Node n = sc.light_nodes[cur];
-        if (!test_box || box_hit(n, ray, inv, tmin, lh.t)) {
-            if (n.b & LEAF_BIT) {
-                const uint32_t cnt = n.b & ~LEAF_BIT;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    const Light& l = sc.lights[sc.light_slot[n.a + k]];
-                    float        t;
-                    if (sphere_t(l.w2o, ray, tmin, lh.t, t)) {
-                        lh.hit = true;
-                        lh.t   = t;
-                        lh.L   = l.radiance;
-                        lh.env = -1;
-                    }
-                }
-            } else {
-                walk_defer(w, n.b);
-                cur      = n.a & CHILD_MASK;
-                test_box = true;
-                continue;
-            }
-        }
-        if (!walk_next(w, ray.d, cur)) break;
-        test_box = true;
-    }
-    return lh;
+    return sc.stackless ? light_bvh_closest<true>(sc, ray, tmin, lh, st) : light_bvh_closest<false>(sc, ray, tmin, lh, st);
 }
 
 __device__ __forceinline__ rgb light_hit_L(const Scene& sc, const LightHit& lh, f3 dir, const Rsq& q)
@@ -908,21 +934,11 @@ __device__ __forceinline__ rgb light_hit_L(const Scene& sc, const LightHit& lh, 
     return (lh.env >= 0) ? env_radiance(sc.envs[lh.env], dir, q) : lh.L;
 }
 
-__device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+template <bool SL>
+__device__ __forceinline__ bool light_bvh_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
-    if (sc.n_light_nodes == 0) return false; // environment lights never occlude
-    if (sc.n_light_nodes == 1) {
-        const Node     n   = uload_node(sc.light_nodes);
-        const uint32_t cnt = n.b & ~LEAF_BIT;
-        for (uint32_t k = 0; k < cnt; ++k) {
-            const aff w2o = uload_aff(&sc.lights[uload_u32(sc.light_slot + n.a + k)].w2o);
-            float     t;
-            if (sphere_t(w2o, ray, tmin, tmax, t)) return true;
-        }
-        return false;
-    }
     const f3 inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    BinWalk  w   = bin_walk(st, sc.light_nodes, sc.light_parents, sc.stackless, false);
+    BinWalk<SL> w = bin_walk<SL>(st, sc.light_nodes, sc.light_parents, false, ray.d);
     uint32_t cur = 0;
     bool     test_box = false;
     while (true) {
@@ -946,6 +962,22 @@ __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, floa
         test_box = true;
     }
     return false;
+}
+
+__device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    if (sc.n_light_nodes == 0) return false; // environment lights never occlude
+    if (sc.n_light_nodes == 1) {
+        const Node     n   = uload_node(sc.light_nodes);
+        const uint32_t cnt = n.b & ~LEAF_BIT;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const aff w2o = uload_aff(&sc.lights[uload_u32(sc.light_slot + n.a + k)].w2o);
+            float     t;
+            if (sphere_t(w2o, ray, tmin, tmax, t)) return true;
+        }
+        return false;
+    }
+    return sc.stackless ? light_bvh_any<true>(sc, ray, tmin, tmax, st) : light_bvh_any<false>(sc, ray, tmin, tmax, st);
 }
 
 // Scene::intersect_p (base/Scene.h:79)

@@ -29,7 +29,10 @@ struct SpError : std::runtime_error {
 };
 
 // ---- host versions of the reference's vector ops that need RSQRTSS ----------------------------
-inline float host_rsqrt(float a) { return spm::rsqrt_newton(a, spm::rsqrtss_host(a)); }
+// RSQRTSS of the host CPU, or -- after sp_rsqrt_table_set -- of the CPU whose table was given
+// (sp_rsqrt.cpp), so a scene is built exactly as the reference built it on that CPU.
+float rsqrtss_active(float a);
+inline float host_rsqrt(float a) { return spm::rsqrt_newton(a, rsqrtss_active(a)); }
 inline f3 host_normalize(f3 a) { return spm::scale(a, host_rsqrt(spm::dot(a, a))); }
 
 // Transformation<T> (math/Transformation.h:37): forward and inverse kept side by side.
@@ -205,5 +208,10 @@ struct RsqrtCapture {
     uint32_t              zero_result = 0, denorm_result = 0;
 };
 const RsqrtCapture& rsqrt_capture();
+// The table the device emulates and host_rsqrt uses: the capture, or the installed override.
+const RsqrtCapture& rsqrt_active();
+// Install another CPU's table (entries == nullptr: back to this host's).  Throws SpError when
+// the table is malformed.
+void rsqrt_set_override(const uint32_t* entries, int32_t bits, uint32_t zero_result, uint32_t denorm_result);
 
 } // namespace sph

@@ -9,6 +9,7 @@
 // reproduces RSQRTSS bit for bit with one table load (spm::rsqrtss_emulated).
 #include "sp_host.hpp"
 
+#include <atomic>
 #include <mutex>
 #include <random>
 
@@ -69,6 +70,43 @@ const RsqrtCapture& rsqrt_capture()
         }
     });
     return cap;
+}
+
+namespace {
+std::mutex   g_override_mu;
+RsqrtCapture g_override;                       // valid when g_use_override
+std::atomic<bool> g_use_override{ false };
+} // namespace
+
+const RsqrtCapture& rsqrt_active()
+{
+    if (g_use_override.load(std::memory_order_acquire)) return g_override;
+    return rsqrt_capture();
+}
+
+void rsqrt_set_override(const uint32_t* entries, int32_t bits, uint32_t zero_result, uint32_t denorm_result)
+{
+    std::lock_guard<std::mutex> lk(g_override_mu);
+    if (!entries) {
+        g_use_override.store(false, std::memory_order_release);
+        return;
+    }
+    if (bits < 1 || bits > 23) throw SpError(SP_ERR_ARG, "RSQRTSS table: bits must be 1..23");
+    g_use_override.store(false, std::memory_order_release);
+    g_override.bits          = bits;
+    g_override.entries.assign(entries, entries + (size_t(2) << bits));
+    g_override.zero_result   = zero_result;
+    g_override.denorm_result = denorm_result;
+    g_override.verified      = true; // as given: the table of the CPU that produced the reference
+    g_use_override.store(true, std::memory_order_release);
+}
+
+float rsqrtss_active(float a)
+{
+    if (!g_use_override.load(std::memory_order_acquire)) return spm::rsqrtss_host(a);
+    const spm::RsqrtTable t{ g_override.entries.data(), g_override.bits, g_override.zero_result,
+                             g_override.denorm_result };
+    return spm::rsqrtss_emulated(a, t);
 }
 
 } // namespace sph

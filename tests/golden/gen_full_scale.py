@@ -14,7 +14,9 @@ tiles is rendered at the config's spp:
      random tiles (seeded);
   3. those tiles are rendered at the config's spp and stored with the mesh generator's
      parameters and the SHA-256 of the generated mesh file, so a test can prove it rebuilt the
-     same scene before comparing.
+     same scene before comparing, and with this CPU's RSQRTSS table: the reference normalises
+     with RSQRTSS (math/Math.h:205), whose outputs differ between CPU vendors, so its image is
+     this CPU's; a test on another machine installs the table (sp_rsqrt_table_set) first.
 
 Run in the build container (the reference sources are needed for oracle/_ref):
     python tests/golden/gen_full_scale.py            # both scenes
@@ -56,6 +58,17 @@ def sha256(path: str) -> str:
         for b in iter(lambda: fh.read(1 << 24), b""):
             h.update(b)
     return h.hexdigest()
+
+
+def host_cpu() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def ref_lib():
@@ -153,11 +166,14 @@ def generate(name: str, workdir: str, threads: int) -> str:
     out = render(L, sc, integ, spp, ids, threads)
     print(f"[{name}] {ids.size} tiles at {spp} spp ({time.time() - t1:.0f} s)", flush=True)
     L.ref_scene_free(sc)
+    rs = sp.rsqrt_table()  # the reference ran with this host's RSQRTSS
     dst = os.path.join(GOLDEN, f"{name}_full_tiles.npz")
     np.savez_compressed(dst, tile_ids=ids, kinds=kinds, radiance=out, width=w, height=h, spp=spp, integrator=integ,
                         writer=cfg["writer"], writer_kw=repr(cfg["kw"]), scene_file=cfg["file"],
                         mesh_file=cfg["mesh"], mesh_sha256=digest,
                         bvh_ref=json.dumps(depth_ref), bvh_sah=json.dumps(depth_sah),
+                        rsqrt_entries=rs["entries"], rsqrt_bits=rs["bits"], rsqrt_zero=rs["zero_result"],
+                        rsqrt_denorm=rs["denorm_result"], host_cpu=host_cpu(),
                         generator="tests/golden/gen_full_scale.py (oracle/_ref = reference sources)")
     print(f"[{name}] wrote {dst} ({time.time() - t0:.0f} s total)", flush=True)
     return dst

@@ -13,7 +13,10 @@ the device built (depth, nodes, slots: identical to the host build recorded with
 and the traversal-stack depth the render used.
 
 The scene is regenerated from the recorded mesh parameters; its SHA-256 must match the one
-recorded, so the comparison is against the same triangles.
+recorded, so the comparison is against the same triangles.  The goldens were made on the build
+container's CPU: the reference normalises with RSQRTSS, whose outputs differ between CPU vendors,
+so these tests install that CPU's recorded RSQRTSS table (sp_rsqrt_table_set) for the scene
+build on the host and for the device's emulation.
 """
 import ast
 import hashlib
@@ -47,11 +50,23 @@ def _sha256(path):
 _scenes = {}
 
 
+@pytest.fixture(scope="module", autouse=True)
+def golden_cpu_rsqrt():
+    """The goldens' RSQRTSS for every scene this module builds and uploads; host's afterwards."""
+    g = np.load(os.path.join(GOLD, "lucy_full_tiles.npz"))
+    sp.set_rsqrt_table({"entries": g["rsqrt_entries"], "bits": int(g["rsqrt_bits"]),
+                        "zero_result": int(g["rsqrt_zero"]), "denorm_result": int(g["rsqrt_denorm"])})
+    yield
+    sp.set_rsqrt_table(None)
+    _scenes.clear()
+
+
 def full_scene(name):
     """(golden dict, sp.Scene at the config's resolution) -- loaded once per session."""
     if name not in _scenes:
         from simplepath_amd import scenes
         g = dict(np.load(os.path.join(GOLD, f"{name}_full_tiles.npz")))
+        assert np.array_equal(g["rsqrt_entries"], sp.rsqrt_table()["entries"])
         kw = ast.literal_eval(str(g["writer_kw"]))  # a dict literal written by the generator
         path = getattr(scenes, str(g["writer"]))(WORKDIR, **kw)
         mesh = os.path.join(WORKDIR, str(g["mesh_file"]))

@@ -35,3 +35,40 @@ def test_rsqrt_table_verified_against_host_instruction():
         a = np.float32(x)
         newton = np.float32(np.float32(1.5) * r32) + np.float32(np.float32(np.float32(a * np.float32(-0.5)) * r32) * np.float32(r32 * r32))
         assert np.float32(L.orc_rsqrt(float(x))) == newton
+
+
+def test_rsqrt_table_override_round_trip(scene_dir):
+    """sp_rsqrt_table_set: building a scene with this host's own table installed as an override
+    (table emulation) gives the same bits as the RSQRTSS instruction; a different table changes the
+    host-built normals (it is really used); NULL restores the host's table."""
+    import os
+
+    import simplepath_amd as sp
+
+    path = os.path.join(scene_dir, "bunny.sp")
+
+    def normals():
+        s = sp.Scene.from_file(path)
+        d = s.desc()
+        n = np.ctypeslib.as_array(d.normals, shape=(d.info.num_vertices, 3)).copy()
+        cam = np.array(list(d.camera.transform.vx) + list(d.camera.transform.vz))
+        return n, cam
+
+    base_n, base_cam = normals()
+    t = sp.rsqrt_table()
+    assert t["entries"].size == 2 << t["bits"]
+    try:
+        sp.set_rsqrt_table(t)
+        n, cam = normals()
+        assert np.array_equal(n.view(np.uint32), base_n.view(np.uint32))
+        assert np.array_equal(cam, base_cam)
+        other = dict(t, entries=t["entries"] + np.uint32(1))  # a CPU whose estimates are 1 ulp higher
+        sp.set_rsqrt_table(other)
+        assert np.array_equal(sp.rsqrt_table()["entries"], other["entries"])
+        n2, _ = normals()
+        assert not np.array_equal(n2.view(np.uint32), base_n.view(np.uint32))
+    finally:
+        sp.set_rsqrt_table(None)
+    assert np.array_equal(sp.rsqrt_table()["entries"], t["entries"])
+    n3, _ = normals()
+    assert np.array_equal(n3.view(np.uint32), base_n.view(np.uint32))
