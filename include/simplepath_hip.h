@@ -11,6 +11,8 @@
  *
  *   sp_scene_load / sp_scene_load_string  base/FileParser.cpp:929 `sp::parse_file`
  *                                         + base/Scene.h:59 `Scene::Scene` (accelerators)
+ *   sp_scene_from_desc                    base/Scene.h:59 `Scene::Scene` from an already-built
+ *                                         scene (main.cpp:368-395 holds one)
  *   sp_scene_get_info                     base/Scene.h:90-96 (image_width, image_height,
  *                                         russian_roulette_depth, max_depth, integrator_type)
  *   sp_scene_get_desc                     the primitive / light / material / camera state
@@ -231,8 +233,15 @@ int  sp_string_to_integrator(const char* name, int32_t* out);
 
 int  sp_scene_load(const char* path, sp_scene** out);
 int  sp_scene_load_string(const char* text, const char* base_dir, sp_scene** out);
+/* Build a scene from a caller's flattened scene (a host that already parsed its scene, e.g.
+ * the reference's main.cpp:368-395 sp::Scene): every array is copied and validated; nothing is
+ * re-parsed.  Layout as sp_scene_get_desc returns it (world-space mesh, Scene::m_geometry order,
+ * camera transform for film_width x film_height).  sp_scene_set_resolution can then not change
+ * the image size (the camera transform fixes it). */
+int  sp_scene_from_desc(const sp_scene_desc* desc, sp_scene** out);
 void sp_scene_free(sp_scene* scene);
 int  sp_scene_get_info(const sp_scene* scene, sp_scene_info* out);
+/* Arrays in *out are owned by the scene: valid until sp_scene_free or sp_scene_set_resolution. */
 int  sp_scene_get_desc(const sp_scene* scene, sp_scene_desc* out);
 /* Override image size after load (camera rebuilt as FileParser would with these values). */
 int  sp_scene_set_resolution(sp_scene* scene, int32_t width, int32_t height);

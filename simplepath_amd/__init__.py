@@ -71,6 +71,13 @@ class Scene:
         check(lib().sp_scene_load_string(text.encode(), base_dir.encode(), C.byref(h)))
         return cls(h)
 
+    @classmethod
+    def from_desc(cls, desc: _abi.sp_scene_desc) -> "Scene":
+        """Scene::Scene from an already-built, flattened scene (sp_scene_from_desc: copied)."""
+        h = C.c_void_p()
+        check(lib().sp_scene_from_desc(C.byref(desc), C.byref(h)))
+        return cls(h)
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h and _abi._lib is not None:

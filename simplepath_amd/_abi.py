@@ -114,6 +114,7 @@ SIGNATURES = {
     "sp_string_to_integrator": (C.c_int, [C.c_char_p, C.POINTER(C.c_int32)]),
     "sp_scene_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
     "sp_scene_load_string": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "sp_scene_from_desc": (C.c_int, [C.POINTER(sp_scene_desc), C.POINTER(C.c_void_p)]),
     "sp_scene_free": (None, [C.c_void_p]),
     "sp_scene_get_info": (C.c_int, [C.c_void_p, C.POINTER(sp_scene_info)]),
     "sp_scene_get_desc": (C.c_int, [C.c_void_p, C.POINTER(sp_scene_desc)]),

@@ -171,6 +171,7 @@ struct sp_scene {
     std::unique_ptr<sph::Scene> host;
     sp_scene_desc               desc{};
     std::vector<sp_env_image>   env_descs; // desc.env_images
+    std::vector<sp_material_desc> mat_descs; // desc.materials
     // device residency
     int                  device   = -1;
     int                  bvh_mode = -1;
@@ -318,15 +319,11 @@ void fill_desc(sp_scene* s)
         put(x.world_to_light.vz, e.world_to_light.vz);
         s->env_descs.push_back(x);
     }
+    s->mat_descs.clear();
+    for (const auto& m : h.materials) s->mat_descs.push_back(m.d);
+    d.materials      = s->mat_descs.empty() ? nullptr : s->mat_descs.data();
     d.env_images     = s->env_descs.empty() ? nullptr : s->env_descs.data();
     d.num_env_images = static_cast<int32_t>(s->env_descs.size());
-}
-
-std::vector<sp_material_desc> material_descs(const sph::Scene& h)
-{
-    std::vector<sp_material_desc> m;
-    for (auto& x : h.materials) m.push_back(x.d);
-    return m;
 }
 
 int wrap_load(std::unique_ptr<sph::Scene> (*fn)(const std::string&, const std::string&), const std::string& a,
@@ -395,16 +392,112 @@ int sp_scene_get_info(const sp_scene* scene, sp_scene_info* out)
 int sp_scene_get_desc(const sp_scene* scene, sp_scene_desc* out)
 {
     if (!scene || !out) return fail(SP_ERR_ARG, "null argument");
-    static thread_local std::vector<sp_material_desc> mats;
-    mats       = material_descs(*scene->host);
-    *out       = scene->desc;
-    out->materials = mats.empty() ? nullptr : mats.data();
+    *out = scene->desc; // arrays owned by the scene: valid until sp_scene_free
     return SP_OK;
+}
+
+// A host that already built its scene (the reference's main.cpp:368-395 holds an sp::Scene)
+// hands it over flattened; nothing is re-parsed.  Every array is copied and checked.
+static int scene_from_desc_impl(const sp_scene_desc* d, sp_scene** out)
+{
+    if (!d || !out) return fail(SP_ERR_ARG, "null argument");
+    const sp_scene_info& in = d->info;
+    if (in.image_width <= 0 || in.image_height <= 0 || in.image_width > 65535 || in.image_height > 65535)
+        return fail(SP_ERR_ARG, "sp_scene_desc: bad image size");
+    if (in.num_triangles < 0 || in.num_vertices < 0 || in.num_shapes < 0 || in.num_lights < 0 || in.num_materials < 0 ||
+        d->num_prims < 0 || d->num_env_images < 0)
+        return fail(SP_ERR_ARG, "sp_scene_desc: negative count");
+    auto need = [](const void* p, int64_t n) { return n == 0 || p != nullptr; };
+    if (!need(d->vertices, in.num_vertices) || !need(d->normals, in.num_vertices) || !need(d->indices, in.num_triangles) ||
+        !need(d->tri_material, in.num_triangles) || !need(d->shapes, in.num_shapes) || !need(d->prim_kind, d->num_prims) ||
+        !need(d->prim_index, d->num_prims) || !need(d->lights, in.num_lights) || !need(d->materials, in.num_materials) ||
+        !need(d->env_images, d->num_env_images))
+        return fail(SP_ERR_ARG, "sp_scene_desc: null array with a nonzero count");
+    if (in.integrator_type < SP_INTEGRATOR_NOT_SPECIFIED || in.integrator_type > SP_INTEGRATOR_WHITTED)
+        return fail(SP_ERR_ARG, "sp_scene_desc: unknown integrator type");
+    auto h             = std::make_unique<sph::Scene>();
+    h->image_width     = in.image_width;
+    h->image_height    = in.image_height;
+    h->rr_depth        = in.russian_roulette_depth;
+    h->max_depth       = in.max_depth;
+    h->integrator      = in.integrator_type;
+    h->output_file_name = std::string(in.output_file_name, strnlen(in.output_file_name, sizeof(in.output_file_name)));
+    h->has_camera      = true;
+    h->camera_fixed    = true;
+    h->camera          = from_desc(d->camera.transform);
+    h->vertices.resize((size_t)in.num_vertices);
+    h->normals.resize((size_t)in.num_vertices);
+    for (int32_t i = 0; i < in.num_vertices; ++i) {
+        h->vertices[i] = spm::mk(d->vertices[3 * i], d->vertices[3 * i + 1], d->vertices[3 * i + 2]);
+        h->normals[i]  = spm::mk(d->normals[3 * i], d->normals[3 * i + 1], d->normals[3 * i + 2]);
+    }
+    h->indices.assign(d->indices, d->indices + (size_t)in.num_triangles * 3);
+    for (uint32_t v : h->indices)
+        if (v >= (uint32_t)in.num_vertices) return fail(SP_ERR_ARG, "sp_scene_desc: vertex index out of range");
+    h->tri_material.assign(d->tri_material, d->tri_material + in.num_triangles);
+    for (int32_t m : h->tri_material)
+        if (m < 0 || m >= in.num_materials) return fail(SP_ERR_ARG, "sp_scene_desc: triangle material out of range");
+    h->shapes.assign(d->shapes, d->shapes + in.num_shapes);
+    for (const auto& x : h->shapes) {
+        if (x.kind != SP_PRIM_SPHERE && x.kind != SP_PRIM_PLANE) return fail(SP_ERR_ARG, "sp_scene_desc: bad shape kind");
+        if (x.material < 0 || x.material >= in.num_materials) return fail(SP_ERR_ARG, "sp_scene_desc: shape material out of range");
+    }
+    h->prim_kind.assign(d->prim_kind, d->prim_kind + d->num_prims);
+    h->prim_index.assign(d->prim_index, d->prim_index + d->num_prims);
+    for (int64_t i = 0; i < d->num_prims; ++i) {
+        const int k = h->prim_kind[i], x = h->prim_index[i];
+        const int n = (k == SP_PRIM_TRIANGLE) ? in.num_triangles : in.num_shapes;
+        if ((k != SP_PRIM_TRIANGLE && k != SP_PRIM_SPHERE && k != SP_PRIM_PLANE) || x < 0 || x >= n ||
+            (k != SP_PRIM_TRIANGLE && h->shapes[x].kind != k))
+            return fail(SP_ERR_ARG, "sp_scene_desc: bad primitive reference");
+    }
+    for (int32_t i = 0; i < in.num_materials; ++i) {
+        const sp_material_desc& m = d->materials[i];
+        if (m.kind < SP_MAT_LAMBERTIAN || m.kind > SP_MAT_CLEARCOAT ||
+            (m.kind == SP_MAT_CLEARCOAT && (m.base < 0 || m.base >= in.num_materials)))
+            return fail(SP_ERR_ARG, "sp_scene_desc: bad material");
+        h->materials.push_back(sph::Material{ m });
+        h->material_names.push_back(std::string());
+    }
+    for (int32_t i = 0; i < d->num_env_images; ++i) {
+        const sp_env_image& e = d->env_images[i];
+        if (e.width <= 0 || e.height <= 0 || !e.pixels) return fail(SP_ERR_ARG, "sp_scene_desc: bad environment image");
+        sph::EnvImage x;
+        x.width        = e.width;
+        x.height       = e.height;
+        x.pixels.assign(e.pixels, e.pixels + (size_t)e.width * e.height * 3);
+        x.max_radiance = e.max_radiance;
+        x.light_to_world = from_desc(e.light_to_world);
+        x.world_to_light = from_desc(e.world_to_light);
+        h->env_images.push_back(std::move(x));
+    }
+    h->lights.assign(d->lights, d->lights + in.num_lights);
+    for (const auto& l : h->lights) {
+        if (l.kind < SP_LIGHT_SPHERE || l.kind > SP_LIGHT_IMAGE_ENVIRONMENT) return fail(SP_ERR_ARG, "sp_scene_desc: bad light kind");
+        if (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT && (l.image < 0 || l.image >= d->num_env_images))
+            return fail(SP_ERR_ARG, "sp_scene_desc: light image out of range");
+    }
+    auto* s = new sp_scene;
+    s->host = std::move(h);
+    fill_desc(s);
+    *out = s;
+    return SP_OK;
+}
+
+int sp_scene_from_desc(const sp_scene_desc* d, sp_scene** out)
+{
+    try {
+        return scene_from_desc_impl(d, out);
+    } catch (const std::exception& e) {
+        return fail(SP_ERR_ARG, std::string("sp_scene_from_desc: ") + e.what());
+    }
 }
 
 int sp_scene_set_resolution(sp_scene* scene, int32_t width, int32_t height)
 {
     if (!scene || width <= 0 || height <= 0 || width > 65535 || height > 65535) return fail(SP_ERR_ARG, "bad resolution");
+    if (scene->host->camera_fixed && (width != scene->host->image_width || height != scene->host->image_height))
+        return fail(SP_ERR_STATE, "scene built from a descriptor: its camera transform fixes the image size");
     scene->host->image_width  = width;
     scene->host->image_height = height;
     scene->host->rebuild_camera();

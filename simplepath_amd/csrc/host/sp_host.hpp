@@ -103,6 +103,7 @@ struct Scene {
     int         integrator   = SP_INTEGRATOR_NOT_SPECIFIED;
     std::string output_file_name;
     bool        has_camera = false;
+    bool        camera_fixed = false; // built from a caller's sp_scene_desc: the transform is given
     // camera parameters kept so the resolution can be overridden
     f3    cam_origin{}, cam_look_at{}, cam_up{};
     float cam_fov_deg = 45.0f;

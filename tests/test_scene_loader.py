@@ -173,3 +173,47 @@ def test_degenerate_strip_bvh_is_stackless(scene_dir):
     assert sah["depth"] < 64 and sah["stack_depth"] == max(sah["depth"], sah["wide_depth"], sah["light_depth"]) + 1
     b = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp")).bvh_build_info(1)
     assert b["stack_depth"] == b["depth"] + 1
+
+
+@pytest.mark.parametrize("name", ["bunny.sp", "material_spheres_ibl.sp", "closed_room.sp"])
+def test_scene_from_desc_round_trip(scene_dir, name):
+    # sp_scene_from_desc: a host-built scene handed over flattened gives back the same scene
+    # (same desc arrays) and the same image on the oracle
+    from tests import _oracle
+    a = sp.Scene.from_file(os.path.join(scene_dir, name))
+    a.set_resolution(24, 16)
+    da = a.desc()
+    b = sp.Scene.from_desc(da)
+    db = b.desc()
+    ia, ib = da.info, db.info
+    for f, _ in type(ia)._fields_:
+        assert getattr(ia, f) == getattr(ib, f), f
+    assert bytes(da.camera) == bytes(db.camera)
+    nv, nt = ia.num_vertices, ia.num_triangles
+    for field, shape in [("vertices", (nv, 3)), ("normals", (nv, 3)), ("indices", (nt, 3)), ("tri_material", (nt,)),
+                         ("prim_kind", (da.num_prims,)), ("prim_index", (da.num_prims,))]:
+        if np.prod(shape) == 0:
+            continue
+        x = np.ctypeslib.as_array(getattr(da, field), shape=shape)
+        y = np.ctypeslib.as_array(getattr(db, field), shape=shape)
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), field
+    for k in range(ia.num_lights):
+        assert bytes(da.lights[k]) == bytes(db.lights[k])
+    for k in range(ia.num_materials):
+        assert bytes(da.materials[k]) == bytes(db.materials[k])
+    ra, _ = _oracle.render(a, 6, 2, threads=4, variant="spm")
+    rb, _ = _oracle.render(b, 6, 2, threads=4, variant="spm")
+    assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32))
+    with pytest.raises(sp.SimplePathError):  # the camera transform fixes the image size
+        b.set_resolution(32, 16)
+
+
+def test_scene_from_desc_validates(scene_dir):
+    a = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp"))
+    d = a.desc()
+    bad = np.ctypeslib.as_array(d.indices, shape=(d.info.num_triangles * 3,)).copy()
+    bad[7] = d.info.num_vertices  # out of range
+    d.indices = bad.ctypes.data_as(type(d.indices))
+    with pytest.raises(sp.SimplePathError) as e:
+        sp.Scene.from_desc(d)
+    assert e.value.code == -3 and "vertex index" in str(e.value)
