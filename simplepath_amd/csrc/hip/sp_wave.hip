@@ -28,7 +28,10 @@
 //   {contrib.rgb, tmax} | queue[n] u32 | mt[tile][buf][312][64] u64 (as in the megakernel).
 // RNG draw-ahead window (sp_path.hpp Rng): off in the wavefront kernels, where it measured
 // 1-2 % slower (it pays off in the megakernel, 2 words ahead).
-#define SP_RNG_PF 0
+#ifndef SP_WAVE_RNG_PF
+#define SP_WAVE_RNG_PF 0
+#endif
+#define SP_RNG_PF SP_WAVE_RNG_PF
 #include "sp_path.hpp"
 #include "sp_wave.hpp"
 
