@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "pmc_valu_bench_bunny.json"),
+                    help="tools/pmc_valu.py output of a PMC pass of this workload (VALU-issue roofline)")
     a = ap.parse_args()
     sc = SCENES[a.scene]
     a.width = a.width or sc["w"]
@@ -299,6 +301,28 @@ def stage_bytes(st, pixels):
     }
 
 
+def valu_of(args, kernel):
+    """VALU-issue roofline of `kernel` from a committed PMC pass of the same workload
+    (tools/gpu_pmc_valu.sh -> tools/pmc_valu.py): issue cycles of its VALU instructions (f32/int
+    2, f64 4, transcendental 8 cycles per wave-instruction, measured on gfx950) over 1024 SIMDs x
+    its cycles.  None when no pass of this workload is committed."""
+    try:
+        with open(args.valu_json) as fh:
+            vj = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if (vj.get("width"), vj.get("height"), vj.get("spp"), vj.get("scene", "bunny")) != \
+            (args.width, args.height, args.spp, args.scene):
+        return None
+    k = vj.get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"frac": round(k["valu_frac"], 4), "wait_frac": round(k.get("wait_frac", 0.0), 4),
+            "lane_util": round(k.get("lane_util", 0.0), 4), "kernel": kernel,
+            "valu_insts_per_launch": k["valu_insts"], "kernel_ms_profiled": round(k["ms_profiled"], 4),
+            "source": os.path.relpath(args.valu_json, ROOT)}
+
+
 def roofline_of(stats, pixels, args, kernel_ms):
     """Roofline of the dominant kernel: algorithmic bytes per launch / average launch duration
     (HIP events on the render stream, recorded around every launch inside the timed region)."""
@@ -333,9 +357,9 @@ def roofline_of(stats, pixels, args, kernel_ms):
     tot = [sum(s.stage_ms[k] for s in stats) / n for k in range(4)]
     spp = args.spp
     by = stage_bytes(st, pixels)
-    # stage events time part 0; with two parts it holds ceil(tiles / 2) of the interleaved tiles
+    # stage events time part 0, which holds about 1 / parts of the interleaved tiles
     tiles = (pixels + 63) // 64
-    frac0 = 0.5 if st.parts == 2 else 1.0  # blocks of tiles dealt alternately: about half
+    frac0 = 1.0 / max(1, st.parts)  # blocks of tiles dealt round-robin: about 1 / parts
     by = {k: v * frac0 for k, v in by.items()}
     stages = {}
     for k in (1, 2, 3):
@@ -352,7 +376,7 @@ def roofline_of(stats, pixels, args, kernel_ms):
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": names[dom],
             "parts": st.parts, "part0_fraction": round(frac0, 4),
             "kernel_ms": d["ms_per_launch"], "alg_bytes_per_launch": d["alg_bytes_per_launch"],
-            "frame_kernel_ms": round(kernel_ms, 2), "stages": stages}
+            "frame_kernel_ms": round(kernel_ms, 2), "stages": stages, "valu": valu_of(args, names[dom])}
 
 
 def _ref_lib():

@@ -189,9 +189,9 @@ struct sp_scene {
     void*                wave_buf     = nullptr; // wavefront pipeline state (sp_wave.hpp WaveArgs)
     size_t               wave_cap     = 0;
     std::vector<hipEvent_t> stage_ev;            // SP_RENDER_STAGE_TIMING
-    hipStream_t          aux_stream   = nullptr; // second part of the wavefront pipeline
-    hipEvent_t           ev_fork = nullptr, ev_join = nullptr;
-    hipEvent_t           ev_shade[2] = { nullptr, nullptr };
+    hipStream_t          aux_stream[spd::WF_MAX_PARTS - 1] = {}; // parts 1.. of the wavefront pipeline
+    hipEvent_t           ev_fork = nullptr, ev_join[spd::WF_MAX_PARTS - 1] = {};
+    hipEvent_t           ev_shade[spd::WF_MAX_PARTS] = {};
     int                  n_cu         = 0;
     hipEvent_t           ev0 = nullptr, ev1 = nullptr;
     void*                ck_buf     = nullptr; // sample-chunk pipeline: hits, radiance, snapshots
@@ -223,15 +223,20 @@ struct sp_scene {
         wave_cap = 0;
         for (hipEvent_t e : stage_ev) (void)hipEventDestroy(e);
         stage_ev.clear();
-        if (aux_stream) (void)hipStreamDestroy(aux_stream);
+        for (hipStream_t& a : aux_stream) {
+            if (a) (void)hipStreamDestroy(a);
+            a = nullptr;
+        }
         if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
+        for (hipEvent_t& e : ev_join) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
         for (hipEvent_t& e : ev_shade) {
             if (e) (void)hipEventDestroy(e);
             e = nullptr;
         }
-        aux_stream = nullptr;
-        ev_fork = ev_join = nullptr;
+        ev_fork = nullptr;
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (wp_buf) (void)hipFree(wp_buf);
@@ -986,13 +991,16 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         const int per_cu = spd::wave_traverse_blocks_per_cu(s->dev);
         int       n_parts = 2;
         if (const char* v = std::getenv("SP_WAVE_PARTS")) n_parts = std::atoi(v);
-        if (n_parts > 1 && !s->aux_stream) {
-            SP_HIP(hipStreamCreateWithFlags(&s->aux_stream, hipStreamNonBlocking));
+        n_parts = std::max(1, std::min(n_parts, spd::WF_MAX_PARTS));
+        if (!s->ev_fork) {
             SP_HIP(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-            SP_HIP(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
-            SP_HIP(hipEventCreateWithFlags(&s->ev_shade[0], hipEventDisableTiming));
-            SP_HIP(hipEventCreateWithFlags(&s->ev_shade[1], hipEventDisableTiming));
+            for (auto& e : s->ev_shade) SP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
+        for (int k = 0; k + 1 < n_parts; ++k)
+            if (!s->aux_stream[k]) {
+                SP_HIP(hipStreamCreateWithFlags(&s->aux_stream[k], hipStreamNonBlocking));
+                SP_HIP(hipEventCreateWithFlags(&s->ev_join[k], hipEventDisableTiming));
+            }
         const size_t n_ev = timing ? 3 * (size_t)w.spp + 3 : 0;
         while (s->stage_ev.size() < n_ev) {
             hipEvent_t e;
@@ -1021,7 +1029,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             w.pb = 0;
             w.pe = w.n;
             SP_HIP(spd::wave_render(s->dev, w, d_out + (size_t)t0 * 64 * 3, per_cu, s->n_cu, stream,
-                                    timing ? s->stage_ev.data() : nullptr, n_parts > 1 ? s->aux_stream : nullptr,
+                                    timing ? s->stage_ev.data() : nullptr, s->aux_stream, n_parts - 1,
                                     s->ev_fork, s->ev_join, s->ev_shade, &parts_used));
             launches += 3 + 4 * (int)w.spp;
             if (d_diag) {

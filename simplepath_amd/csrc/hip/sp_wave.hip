@@ -56,20 +56,29 @@ struct PixelRef {
     bool     inside;
 };
 
-// Internal slot -> caller's slot.  With two parts the caller's tiles are dealt in blocks of
-// ilv tiles, alternately (part 0 = blocks 0, 2, 4 ..., part 1 = blocks 1, 3, ...), so both parts
-// see a similar mix of cheap (sky) and expensive tiles while neighbouring tiles stay together.
-__host__ __device__ inline int64_t part0_slots(int64_t slots, int64_t ilv)
+// Internal slot -> caller's slot.  With P parts the caller's tiles are dealt in blocks of ilv
+// tiles, round-robin (part k = blocks k, k + P, k + 2P, ...; a last partial block goes to the
+// part whose turn it is), so every part sees a similar mix of cheap (sky) and expensive tiles
+// while neighbouring tiles stay together.  Internal slots hold part 0's tiles, then part 1's, ...
+__host__ __device__ inline int64_t part_slots(int64_t slots, int64_t ilv, int parts, int k)
 {
     const int64_t full = slots / ilv, rem = slots % ilv;
-    return ((full + 1) / 2) * ilv + ((full % 2 == 0) ? rem : 0);
+    const int64_t nb   = (full > k) ? (full - k + parts - 1) / parts : 0;
+    return nb * ilv + ((full % parts == k) ? rem : 0);
 }
 __device__ __forceinline__ int64_t caller_slot(const WaveArgs& w, int64_t slot)
 {
     if (!w.interleave) return slot;
-    const int64_t ilv = w.interleave, p0 = part0_slots(w.n >> 6, ilv);
-    const int64_t s   = slot < p0 ? slot : slot - p0;
-    return (2 * (s / ilv) + (slot < p0 ? 0 : 1)) * ilv + s % ilv;
+    const int64_t ilv = w.interleave, slots = w.n >> 6;
+    int           k   = 0;
+    int64_t       s   = slot;
+    while (k + 1 < w.n_parts) {
+        const int64_t ns = part_slots(slots, ilv, w.n_parts, k);
+        if (s < ns) break;
+        s -= ns;
+        ++k;
+    }
+    return ((s / ilv) * w.n_parts + k) * ilv + s % ilv;
 }
 
 __device__ __forceinline__ PixelRef pixel_of(const Scene& sc, const WaveArgs& w, int64_t p)
@@ -428,16 +437,17 @@ size_t wave_bytes_per_pixel(int n_lights)
 // primary/shade/resolve slots (one per tile) + persistent shadow-wave slots (at most as many)
 // tile slots + persistent shadow-wave slots of both parts (each part's grid is at most
 // ceil(part pixels / WF_BLOCK) blocks of WF_BLOCK / 64 waves)
-size_t wave_stat_bytes(int64_t n) { return (size_t)(2 * (size_t)(n >> 6) + 8) * ST_N * 8; }
-// room for up to two parts (wave_render), each QSEG segments + QSEG counters
+size_t wave_stat_bytes(int64_t n) { return (size_t)(2 * (size_t)(n >> 6) + 8 * WF_MAX_PARTS) * ST_N * 8; }
+// room for up to WF_MAX_PARTS parts (wave_render), each QSEG segments + QSEG counters
 size_t wave_queue_bytes(int64_t n, int n_lights)
 {
-    return 2 * (QSEG * (qseg_cap(n) * (size_t)std::max(1, n_lights) + 64) + QSEG * QSTRIDE) * 4;
+    const size_t L = (size_t)std::max(1, n_lights);
+    return (QSEG * (qseg_cap(n) + (size_t)WF_MAX_PARTS * 64) * L + (size_t)WF_MAX_PARTS * QSEG * QSTRIDE) * 4 + 4096;
 }
 
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
-                       hipStream_t stream, hipEvent_t* ev, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
-                       hipEvent_t* shade_done, int* parts_out)
+                       hipStream_t stream, hipEvent_t* ev, const hipStream_t* aux, int n_aux, hipEvent_t fork,
+                       const hipEvent_t* join, hipEvent_t* shade_done, int* parts_out)
 {
     int  e    = 0;
     auto mark = [&]() {
@@ -447,20 +457,24 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     const size_t rs_lds    = (size_t)(2 << sc.rsqrt_bits) * 4;
     const unsigned grid_all = (unsigned)((w.n + WF_BLOCK - 1) / WF_BLOCK);
 
-    // Parts: contiguous tile ranges with their own queue, each driven by its own stream, so that
-    // one part's traversal kernels (memory-latency bound) overlap the other part's shading
-    // (VALU bound) on the same CUs.
-    const int   parts = (aux && w.n >= 2 * 64 * 256) ? 2 : 1;
+    // Parts: tile sets with their own queues, each driven by its own stream, so that one part's
+    // traversal kernels (memory-latency bound) overlap another part's shading on the same CUs.
+    // At least 256 tiles per part; SP_WAVE_PARTS (via n_aux + 1) sets the number.
+    int parts = 1 + std::max(0, n_aux);
+    while (parts > 1 && w.n < (int64_t)parts * 64 * 256) --parts;
+    parts = std::min(parts, WF_MAX_PARTS);
     if (parts_out) *parts_out = parts;
-    WaveArgs    pw[2];
-    hipStream_t ps[2] = { stream, aux };
+    WaveArgs    pw[WF_MAX_PARTS];
+    hipStream_t ps[WF_MAX_PARTS] = { stream, nullptr, nullptr, nullptr };
+    for (int k = 1; k < parts; ++k) ps[k] = aux[k - 1];
     WaveArgs    wa    = w;
     wa.interleave     = parts > 1 ? interleave_block_env() : 0;
+    wa.n_parts        = parts;
     const int64_t slots = w.n >> 6;
     int64_t       s0    = 0;
     uint32_t*     q     = w.queue;
     for (int k = 0; k < parts; ++k) {
-        const int64_t ns = (k == parts - 1) ? slots - s0 : part0_slots(slots, wa.interleave);
+        const int64_t ns = parts > 1 ? part_slots(slots, wa.interleave, parts, k) : slots;
         pw[k]            = wa;
         pw[k].pb         = s0 * 64;
         pw[k].pe         = (s0 + ns) * 64;
@@ -476,7 +490,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     mark();
     if (parts > 1) {
         (void)hipEventRecord(fork, stream);
-        (void)hipStreamWaitEvent(aux, fork, 0);
+        for (int k = 1; k < parts; ++k) (void)hipStreamWaitEvent(ps[k], fork, 0);
     }
     const uint32_t diag_sample = diag_sample_env();
     // waves per SIMD requested for the shading kernel (register budget vs spills)
@@ -487,20 +501,22 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     case 6: shade = wf_shade<6>; break;
     default: break;
     }
-    unsigned       grid[2], sgrid[2];
-    WaveArgs       pd[2];
+    unsigned       grid[WF_MAX_PARTS], sgrid[WF_MAX_PARTS];
+    WaveArgs       pd[WF_MAX_PARTS];
+    int64_t        sh_slot = w.n >> 6;
     for (int k = 0; k < parts; ++k) {
         grid[k]  = (unsigned)((pw[k].pe - pw[k].pb + WF_BLOCK - 1) / WF_BLOCK);
         // the shadow queue never exceeds the part: a persistent grid sized to fill the chip
         sgrid[k] = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid[k], (int64_t)n_cu * traverse_blocks_per_cu));
         // statistics slots of this part's persistent shadow waves, after the tile slots
-        pw[k].sh_slot0 = (w.n >> 6) + (k == 0 ? 0 : (int64_t)sgrid[0] * (WF_BLOCK / 64));
+        pw[k].sh_slot0 = sh_slot;
+        sh_slot += (int64_t)sgrid[k] * (WF_BLOCK / 64);
         pd[k]      = pw[k]; // diagnostics: only the launches of sample diag_sample record
         pd[k].diag = nullptr;
     }
-    // With two parts the shading kernels alternate (A's shade, then B's, then A's ...) through a
-    // pair of cross-stream events, so each part's traversal kernels run beside the other part's
-    // shading instead of both parts shading at once.
+    // With several parts the shading kernels take turns (part 0's shade, then part 1's, ...,
+    // then part 0's again) through cross-stream events, so each part's traversal kernels run
+    // beside another part's shading instead of all parts shading at once.
     for (uint32_t i = 0; i < w.spp; ++i) {
         for (int k = 0; k < parts; ++k) {
 #ifdef SP_SHADE_PROF // the diag buffer holds the shade timeline only
@@ -512,7 +528,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
             hipStream_t     st = ps[k];
             hipLaunchKernelGGL(wf_primary, dim3(grid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi, i);
             if (k == 0) mark();
-            if (parts > 1 && (k == 1 || i > 0)) (void)hipStreamWaitEvent(st, shade_done[1 - k], 0);
+            if (parts > 1 && (k > 0 || i > 0)) (void)hipStreamWaitEvent(st, shade_done[(k + parts - 1) % parts], 0);
 #ifdef SP_SHADE_PROF
             hipLaunchKernelGGL(shade, dim3(grid[k]), dim3(WF_BLOCK), rs_lds, st, sc, ws, i);
 #else
@@ -525,12 +541,12 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
             if (k == 0) mark();
         }
     }
-    if (parts > 1) {
-        (void)hipEventRecord(join, aux);
-        (void)hipStreamWaitEvent(stream, join, 0);
+    for (int k = 1; k < parts; ++k) {
+        (void)hipEventRecord(join[k - 1], ps[k]);
+        (void)hipStreamWaitEvent(stream, join[k - 1], 0);
     }
     hipLaunchKernelGGL(wf_resolve, dim3(grid_all), dim3(WF_BLOCK), 0, stream, sc, wa, out);
-    const int64_t n_slots = 2 * slots + 8;
+    const int64_t n_slots = 2 * slots + 8 * WF_MAX_PARTS;
     hipLaunchKernelGGL(wf_stats, dim3(64), dim3(WF_BLOCK), 0, stream, w, n_slots);
     mark();
     return hipGetLastError();

@@ -9,7 +9,8 @@ namespace spd {
 struct WaveArgs {
     int64_t             n;         // pixel slots in flight = tiles * 64 (array strides)
     int64_t             pb, pe;    // pixel slot range handled by this launch sequence
-    int32_t             interleave;// >0: tile block size dealt alternately to two parts (caller_slot)
+    int32_t             interleave;// >0: tile block size dealt round-robin to the parts (caller_slot)
+    int32_t             n_parts;   // parts the caller's tiles are dealt to (1..WF_MAX_PARTS)
     const int32_t*      tile_ids;  // nullptr => identity
     int32_t             tiles_x;
     uint32_t            spp;
@@ -30,15 +31,17 @@ struct WaveArgs {
 };
 
 constexpr int WF_MAX_LIGHTS = 32; // light mask is one u32 per pixel
+constexpr int WF_MAX_PARTS  = 4;  // overlapped parts of the wavefront pipeline (streams)
 
 size_t     wave_bytes_per_pixel(int n_lights);
 size_t     wave_stat_bytes(int64_t n);
 size_t     wave_queue_bytes(int64_t n, int n_lights);
 // ev: optional 3 * spp + 3 events recorded around the launches of part 0 (stage timing);
-// aux (may be null): second stream for the overlapped second part, fork/join its events.
+// aux[0..n_aux): streams of the overlapped parts 1.., fork / join[k] their events,
+// shade_done[WF_MAX_PARTS] the shade-alternation events.
 hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int traverse_blocks_per_cu, int n_cu,
-                       hipStream_t stream, hipEvent_t* ev, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
-                       hipEvent_t* shade_done /* [2] */, int* parts_out);
+                       hipStream_t stream, hipEvent_t* ev, const hipStream_t* aux, int n_aux, hipEvent_t fork,
+                       const hipEvent_t* join, hipEvent_t* shade_done, int* parts_out);
 int        wave_traverse_blocks_per_cu(const Scene& sc);
 
 // Wavefront multi-bounce pipeline (sp_wpath.hip): BruteForceIterative(RR), IterativeRRNEE.

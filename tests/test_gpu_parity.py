@@ -180,6 +180,22 @@ def test_wavefront_two_parts(scene_dir, monkeypatch):
     assert np.array_equal(one, w)
 
 
+@pytest.mark.parametrize("parts", ["3", "4"])
+def test_wavefront_more_parts(scene_dir, monkeypatch, parts):
+    # 1600 tiles dealt round-robin in blocks of 240 to 3 or 4 overlapped parts (ragged last block)
+    s = load(scene_dir, "bunny.sp", 512, 200, bvh=0)
+    monkeypatch.setenv("SP_WAVE_PARTS", "1")
+    one, ost = sp.render_tiles(s, "direct_lighting", 1, pipeline="wavefront")
+    monkeypatch.setenv("SP_WAVE_PARTS", parts)
+    many, mst = sp.render_tiles(s, "direct_lighting", 1, pipeline="wavefront")
+    assert ost.parts == 1 and mst.parts == int(parts)
+    assert np.array_equal(one.view(np.uint32), many.view(np.uint32))
+    assert (ost.rays, ost.shadow_rays, ost.rng_draws) == (mst.rays, mst.shadow_rays, mst.rng_draws)
+    ids = np.random.default_rng(7).permutation(one.shape[0]).astype(np.int32)
+    sub, _ = sp.render_tiles(s, "direct_lighting", 1, ids, pipeline="wavefront")
+    assert np.array_equal(sub, one[ids])
+
+
 def test_wavefront_tile_chunks(scene_dir, monkeypatch):
     # a tiny state budget forces several tile chunks per call; result must not change
     s = load(scene_dir, "bunny.sp", 64, 48, bvh=0)

@@ -4,12 +4,13 @@
 The shading kernels do exact glibc-libm arithmetic (f32 + f64) and move few bytes, so their
 roofline is the SIMDs' VALU issue rate, not HBM.  Per launch:
 
-  valu_cycles = 2 * (VALU - F64 - TRANS)   wave64 f32 / int32 / logic: 2 cycles per SIMD (32 lanes/clk;
-                                            MI355X_MICROARCH.md 'v_fma_f32 (wave64) 2 cyc', = the
-                                            157.3 TFLOP/s f32 vector peak)
-              + 4 * (FMA_F64 + ADD_F64 + MUL_F64 + INT64)   half rate (78.6 TFLOP/s f64 vector peak)
-              + 4 * TRANS_F32                               transcendental: quarter lane rate
-              + 8 * TRANS_F64
+  valu_cycles = 2 * (VALU - F64 - TRANS)   wave64 f32 / int32 / logic
+              + 4 * (FMA_F64 + ADD_F64 + MUL_F64 + INT64)
+              + 8 * TRANS_F32
+              + 16 * TRANS_F64
+  cycles per wave-instruction per SIMD measured on gfx950 by tools/ubench/valu_rate.hip
+  (profiles/r02/valu_rate.txt, 4-8 waves per SIMD): v_mul_f32 / v_xor_b32 2.2-2.4, v_mul_f64 /
+  v_add_f64 4.2, v_exp_f32 8.2 (INT64 and f64 transcendentals by analogy: 4 and 16)
   kernel_cycles = GRBM_GUI_ACTIVE / 8     (rocprofv3 sums the 8 XCDs' busy cycles; microarch guide)
   valu_frac   = valu_cycles / (1024 SIMDs * kernel_cycles)
 
@@ -73,7 +74,7 @@ def main():
                                            "SQ_INSTS_VALU_INT64"))
         t32, t64 = m.get("SQ_INSTS_VALU_TRANS_F32", 0.0), m.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
         rest = max(0.0, m["SQ_INSTS_VALU"] - f64 - t32 - t64)
-        vcyc = 2.0 * rest + 4.0 * f64 + 4.0 * t32 + 8.0 * t64
+        vcyc = 2.0 * rest + 4.0 * f64 + 8.0 * t32 + 16.0 * t64
         kcyc = m["GRBM_GUI_ACTIVE"] / 8.0
         d = {"dispatches": len(c["SQ_INSTS_VALU"]), "valu_insts": m["SQ_INSTS_VALU"], "valu_cycles": vcyc,
              "kernel_cycles": kcyc, "valu_frac": vcyc / (N_SIMD * kcyc),
