@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 R=$GRAFT_REPO_ROOT
-OUT=gpurun_out/pmcv
+OUT=gpurun_out/pmcv_${TAG:-bench}
 mkdir -p $OUT
 export TMPDIR=/tmp
 ARGS="--steps 1 --warmup 0 --no-cpu --spp ${SPP:-256} ${BENCH_ARGS:-}"

@@ -17,11 +17,12 @@ import sys
 
 
 def kernel_key(name):
-    """'void spd::wf_shade<4>(spd::Scene, ...)' -> 'spd::wf_shade' (template instances merged)."""
-    k = name.split("(")[0]
+    """'void spd::wf_shade<4>(spd::Scene, ...)' -> 'wf_shade' (template instances merged;
+    '(anonymous namespace)::' dropped)."""
+    k = name.replace("(anonymous namespace)::", "")
     if k.startswith("void "):
         k = k[5:]
-    return k.split("<")[0]
+    return k.split("(")[0].split("<")[0].replace("spd::", "")
 
 
 def per_kernel(root, counter):
@@ -40,7 +41,7 @@ def main():
     write = per_kernel(os.path.join(root, "p2"), "WRITE_SIZE")
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith("spd::"):
+        if k.startswith("__amd") or "at::" in k:
             continue
         f, wr = fetch.get(k, []), write.get(k, [])
         n = max(len(f), len(wr), 1)

@@ -33,10 +33,12 @@ N_SIMD = 1024  # 256 CUs x 4 SIMDs
 
 
 def kernel_key(name):
-    k = name.split("(")[0]
+    """'void spd::wf_shade<4>(spd::Scene, ...)' -> 'wf_shade' (template instances merged;
+    '(anonymous namespace)::' dropped)."""
+    k = name.replace("(anonymous namespace)::", "")
     if k.startswith("void "):
         k = k[5:]
-    return k.split("<")[0].replace("spd::", "")
+    return k.split("(")[0].split("<")[0].replace("spd::", "")
 
 
 def load(root):
