@@ -137,15 +137,24 @@ def main():
     import torch
 
     dist = None
+    # SP_BENCH_SHARED_DEVICE=1 (test hook): every rank renders on cuda:0 and the ranks talk over
+    # gloo with host copies -- the N>1 flow on a one-GPU box (RCCL needs one GPU per rank)
+    shared = world > 1 and os.environ.get("SP_BENCH_SHARED_DEVICE") == "1"
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if shared:
+            local = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         world = dist.get_world_size()
     else:
         torch.cuda.set_device(0)
         local = 0
+    cdev = "cpu" if shared else f"cuda:{local}"  # where the collectives' tensors live
 
     import simplepath_amd as sp
     from simplepath_amd import scenes
@@ -174,8 +183,8 @@ def main():
     out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
     gathered, frame = None, None
     if dist is not None and rank == 0:
-        gathered = [torch.zeros_like(out) for _ in range(world)]
-        frame = torch.zeros((n_tiles, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
+        gathered = [torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=cdev) for _ in range(world)]
+        frame = torch.zeros((n_tiles, 64, 3), dtype=torch.float32, device=cdev)
     stream = torch.cuda.current_stream().cuda_stream
     gather_ms = []
 
@@ -185,7 +194,7 @@ def main():
         if dist is not None:  # single RCCL gather of the tile buffers at frame end
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            shard.gather_frame(out, n_tiles, rank, world, dist, gathered, frame)
+            shard.gather_frame(out if not shared else out.cpu(), n_tiles, rank, world, dist, gathered, frame)
             e1.record()
             gather_ms.append((e0, e1))
         return st
@@ -213,13 +222,13 @@ def main():
     g_ms = sum(a.elapsed_time(b) for a, b in timed_gathers) / len(timed_gathers) if timed_gathers else 0.0
     rank_info = None
     if dist is not None:
-        t = torch.tensor([elapsed, float(rays), float(samples), float(draws)], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed, float(rays), float(samples), float(draws)], dtype=torch.float64, device=cdev)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0])
         rays, samples, draws = float(t[1]), float(t[2]), float(t[3])
-        mine = torch.tensor([float(len(my_tiles)), g_ms, kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
+        mine = torch.tensor([float(len(my_tiles)), g_ms, kernel_ms], dtype=torch.float64, device=cdev)
         every = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(every, mine)
         rank_info = [{"rank": r, "tiles": int(v[0]), "gather_ms": round(float(v[1]), 3),
@@ -278,6 +287,8 @@ def main():
     }
     if dist is not None:
         line["world_size"] = world
+        if shared:
+            line["test_shared_device"] = True  # not a multi-GPU measurement
         line["gather_ms"] = round(g_ms, 3)
         line["ranks"] = rank_info
     print(json.dumps(line), flush=True)
