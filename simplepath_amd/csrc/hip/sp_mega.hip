@@ -15,6 +15,15 @@ static bool regen_env()
     return v ? std::atoi(v) != 0 : false;
 }
 
+// The lock-step IterativeRRNEE megakernel runs with the selection-weight estimates merged across
+// call sites (sp_path.hpp integrate_rrnee_merged; identical images): 440 vs 395 Mrays/s on elf
+// 1024^2 x 16 spp.  SP_RRNEE_MERGED=0 selects the per-call-site form for comparison.
+static bool rrnee_merged_env()
+{
+    const char* v = std::getenv("SP_RRNEE_MERGED");
+    return v ? std::atoi(v) != 0 : true;
+}
+
 // variant = requested waves per SIMD for __launch_bounds__ (1..4, DirectLighting only); 0 = default
 KernelFn select_kernel(int integ, int variant)
 {
@@ -23,7 +32,7 @@ KernelFn select_kernel(int integ, int variant)
     case SP_INTEGRATOR_WHITTED: return mega_recursive(integ);
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE:
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: return mega_iterative(integ, regen_env());
-    case SP_INTEGRATOR_ITERATIVE_RRNEE: return mega_rrnee(regen_env());
+    case SP_INTEGRATOR_ITERATIVE_RRNEE: return mega_rrnee(regen_env(), rrnee_merged_env());
     case SP_INTEGRATOR_MANDELBROT: return mega_mandelbrot();
     default: return mega_direct(variant);
     }

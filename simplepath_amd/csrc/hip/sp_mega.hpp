@@ -8,6 +8,9 @@
 namespace spd {
 
 constexpr int WAVES_PER_BLOCK = 4;
+// IterativeRRNEE with its selection-weight estimates merged across call sites (sp_path.hpp
+// integrate_rrnee_merged): same image, another instantiation of the kernel templates.
+constexpr int INTEG_RRNEE_MERGED = 0x100 | SP_INTEGRATOR_ITERATIVE_RRNEE;
 
 template <int INTEG>
 __device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
@@ -16,6 +19,7 @@ __device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
     else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE) return integrate_iterative<false>(c, ray);
     else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR) return integrate_iterative<true>(c, ray);
     else if constexpr (INTEG == SP_INTEGRATOR_ITERATIVE_RRNEE) return integrate_rrnee(c, ray);
+    else if constexpr (INTEG == INTEG_RRNEE_MERGED) return integrate_rrnee_merged(c, ray);
     else if constexpr (INTEG == SP_INTEGRATOR_WHITTED) return integrate_whitted(c, ray);
     else return integrate_direct(c, ray);
 }
@@ -266,7 +270,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_regen(Sc
 using KernelFn = void (*)(Scene, RenderArgs);
 KernelFn mega_direct(int variant);
 KernelFn mega_iterative(int integ, bool regen);
-KernelFn mega_rrnee(bool regen);
+KernelFn mega_rrnee(bool regen, bool merged);
 KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 

@@ -1032,9 +1032,8 @@ constexpr float k_uniform_hemisphere_pdf = 1.0f / (2.0f * k_pi);
 struct Onb {
     f3 u, v, w;
 };
-__device__ __forceinline__ Onb onb_from_v(f3 n, const Rsq& q)
+__device__ __forceinline__ Onb onb_of_unit(f3 v)
 {
-    const f3    v    = normalize(n, q);
     const float sign = copysign_f(1.0f, v.z);
     const float a    = -1.0f / (sign + v.z);
     const float b    = v.x * v.y * a;
@@ -1046,6 +1045,7 @@ __device__ __forceinline__ Onb onb_from_v(f3 n, const Rsq& q)
     o.w = b1;
     return o;
 }
+__device__ __forceinline__ Onb onb_from_v(f3 n, const Rsq& q) { return onb_of_unit(normalize(n, q)); }
 __device__ __forceinline__ f3 to_world(const Onb& o, f3 a) { return add(add(scale(a.x, o.u), scale(a.y, o.v)), scale(a.z, o.w)); }
 __device__ __forceinline__ f3 to_onb(const Onb& o, f3 a) { return mk(dot(a, o.u), dot(a, o.v), dot(a, o.w)); }
 
@@ -1417,12 +1417,11 @@ __device__ __forceinline__ MSample lambert_sample(const Material& m, Rng& rng)
     return r;
 }
 
-// Local-space sample/eval/pdf of a non-clearcoat material (OneSampleMaterial).
-__device__ __forceinline__ MSample onesample_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+// Local-space sample/eval/pdf of a non-clearcoat material (OneSampleMaterial).  The glossy forms
+// are split at the selection-weight estimate: *_w take the weights glossy_weights produced (the
+// merged multi-bounce integrator runs that estimate once for lanes at different call sites).
+__device__ __forceinline__ MSample onesample_sample_w(const Material& m, f3 wo, const float w[2], Rng& rng, const Rsq& q)
 {
-    if (m.kind == SP_MAT_LAMBERTIAN) return lambert_sample(m, rng);
-    float w[2];
-    glossy_weights(m, wo, rng, q, w);
     const float u   = next1D(rng);
     float       cdf = 0.0f;
     int         sel = 1; // loop falls through only on NaN weights (uninitialised in the reference)
@@ -1468,7 +1467,24 @@ __device__ __forceinline__ MSample onesample_sample(const Material& m, f3 wo, Rn
     out.props = res.props;
     return out;
 }
+__device__ __forceinline__ MSample onesample_sample(const Material& m, f3 wo, Rng& rng, const Rsq& q)
+{
+    if (m.kind == SP_MAT_LAMBERTIAN) return lambert_sample(m, rng);
+    float w[2];
+    glossy_weights(m, wo, rng, q, w);
+    return onesample_sample_w(m, wo, w, rng, q);
+}
 
+__device__ __forceinline__ rgb onesample_eval_w(const Material& m, f3 wo, f3 wi, const float w[2], const Rsq& q)
+{
+    const float p0    = mf_pdf(m, wo, wi, q) * w[0];
+    const float p1    = k_uniform_hemisphere_pdf * w[1];
+    const float inner = (0.0f + p0) + p1;
+    rgb         r     = mkc(0, 0, 0);
+    if (p0 > 0.0f) r = cadd(r, cscale(mf_eval(m, wo, wi, q), balance(p0, inner)));
+    if (p1 > 0.0f) r = cadd(r, cscale(m.lambert_albedo, balance(p1, inner)));
+    return r;
+}
 __device__ __forceinline__ rgb onesample_eval(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
 {
     if (m.kind == SP_MAT_LAMBERTIAN) {
@@ -1481,15 +1497,16 @@ __device__ __forceinline__ rgb onesample_eval(const Material& m, f3 wo, f3 wi, R
     }
     float w[2];
     glossy_weights(m, wo, rng, q, w);
-    const float p0    = mf_pdf(m, wo, wi, q) * w[0];
-    const float p1    = k_uniform_hemisphere_pdf * w[1];
-    const float inner = (0.0f + p0) + p1;
-    rgb         r     = mkc(0, 0, 0);
-    if (p0 > 0.0f) r = cadd(r, cscale(mf_eval(m, wo, wi, q), balance(p0, inner)));
-    if (p1 > 0.0f) r = cadd(r, cscale(m.lambert_albedo, balance(p1, inner)));
-    return r;
+    return onesample_eval_w(m, wo, wi, w, q);
 }
 
+__device__ __forceinline__ float onesample_pdf_w(const Material& m, f3 wo, f3 wi, const float w[2], const Rsq& q)
+{
+    float p = 0.0f;
+    p += w[0] * mf_pdf(m, wo, wi, q);
+    p += w[1] * k_uniform_hemisphere_pdf;
+    return p;
+}
 __device__ __forceinline__ float onesample_pdf(const Material& m, f3 wo, f3 wi, Rng& rng, const Rsq& q)
 {
     if (m.kind == SP_MAT_LAMBERTIAN) {
@@ -1500,10 +1517,7 @@ __device__ __forceinline__ float onesample_pdf(const Material& m, f3 wo, f3 wi, 
     }
     float w[2];
     glossy_weights(m, wo, rng, q, w);
-    float p = 0.0f;
-    p += w[0] * mf_pdf(m, wo, wi, q);
-    p += w[1] * k_uniform_hemisphere_pdf;
-    return p;
+    return onesample_pdf_w(m, wo, wi, w, q);
 }
 
 // Material::sample/eval/pdf incl. ClearcoatMaterial (materials/Material.h:461-529, 723-806)
@@ -1935,6 +1949,236 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
         } else {
             break;
         }
+    }
+    return L;
+}
+
+// IntegratorIterativeRRNEE with the selection-weight estimates merged across call sites.
+// A bounce evaluates the glossy lobe's 16-sample albedo estimate (glossy_weights) at up to four
+// places -- material.sample for the path (Integrator.cpp:573), and per light material.eval,
+// material.pdf and material.sample in estimate_direct_mis (:507-516) -- and the lanes of a wave
+// reach them at different times (occluded shadow rays skip two, lambertian materials all four).
+// Here each lane runs its bounce as a small state machine up to its next estimate; then every
+// lane waiting on one runs the SAME single copy of glossy_weights together, and all continue.
+// Each lane draws and computes exactly what integrate_rrnee does, in the same order (bit-identical:
+// tests/test_gpu_parity.py); only which lanes share an instruction changes.
+enum : int {
+    RB_PATH, RB_PATH_W, RB_PATH_DONE,            // material.sample for the path
+    RB_LIGHT, RB_EVAL_W, RB_EVAL_DONE, RB_PDF_W, RB_PDF_DONE, RB_MIS, RB_MIS_W, RB_MIS_DONE, // per light
+    RB_END
+};
+
+// ClearcoatMaterial::sample's scaling of its base's sample (Material.h:723-760)
+__device__ __forceinline__ MSample coat_wrap(const Material& top, float f, const MSample& b)
+{
+    if (b.pdf == 0.0f) return b;
+    MSample s;
+    s.pdf   = (1.0f - f) * b.pdf;
+    s.color = cmul(csub(mkc(1, 1, 1), cscale(top.coat_color, f)), b.color);
+    s.dir   = b.dir;
+    s.props = b.props;
+    return s;
+}
+// ClearcoatMaterial::sample's specular branch
+__device__ __forceinline__ MSample coat_reflect(const Material& top, float f, f3 wo)
+{
+    MSample s;
+    s.dir   = mk(-wo.x, wo.y, -wo.z);
+    s.color = cdivs(cscale(top.coat_color, f), abs_f(s.dir.y));
+    s.pdf   = f;
+    s.props = PROP_SPECULAR | PROP_REFLECTIVE;
+    return s;
+}
+// OneSampleMaterial::eval / pdf of a lambertian-only material (no weight estimate, no draws)
+__device__ __forceinline__ rgb lambert_eval(const Material& m)
+{
+    const float w     = lambert_only_weight(m);
+    const float p     = k_uniform_hemisphere_pdf * w;
+    const float inner = 0.0f + p;
+    rgb         r     = mkc(0, 0, 0);
+    if (p > 0.0f) r = cadd(r, cscale(m.lambert_albedo, balance(p, inner)));
+    return r;
+}
+__device__ __forceinline__ float lambert_pdf(const Material& m)
+{
+    const float w = lambert_only_weight(m);
+    float       p = 0.0f;
+    p += w * k_uniform_hemisphere_pdf;
+    return p;
+}
+
+__device__ __forceinline__ rgb integrate_rrnee_merged(Ctx& c, Ray ray)
+{
+    const Scene& sc         = c.sc;
+    rgb          throughput = mkc(1, 1, 1);
+    rgb          L          = mkc(0, 0, 0);
+    float        tmin = k_ray_epsilon, tmax = k_infinite;
+    constexpr float rr_cut = 0.1f;
+    for (int depth = 0; depth < sc.max_depth; ++depth) {
+        rng_prepare(c.rng);
+        const Query qr = trace(c, ray, tmin, tmax);
+        if (!qr.geom) {
+            if (qr.lh.hit) L = cadd(L, cmul(throughput, light_hit_L(sc, qr.lh, ray.d, c.q)));
+            break;
+        }
+        const f3        next_o = ray_at(ray, qr.is.t);
+        const f3        n      = qr.is.n;
+        const f3        P      = qr.is.p;
+        const f3        nv     = normalize(n, c.q); // the shading frame is rebuilt from it where used
+        const f3        wo_l   = to_onb(onb_of_unit(nv), neg(ray.d));
+        const Material& top    = sc.materials[qr.is.material];
+        const bool      coat   = top.kind == SP_MAT_CLEARCOAT;
+        const Material& base   = coat ? sc.materials[top.base] : top;
+        const bool      glossy = base.kind != SP_MAT_LAMBERTIAN;
+        const float     fc     = coat ? fresnel_dielectric(wo_l.y, 1.0f, top.coat_ior) : 0.0f;
+
+        int     stage = RB_PATH, li = 0;
+        bool    path_ok = false;
+        MSample s, ms;
+        LSample ls;
+        f3      wi_l = mk(0, 0, 0);
+        rgb     beL = mkc(0, 0, 0), Lr = mkc(0, 0, 0); // material.eval x light radiance
+        bool    eval_black = true;
+        float   bp = 0.0f, lcos = 0.0f;
+        float   w[2] = { 0.0f, 0.0f };
+        while (true) {
+            bool need = false;
+            while (!need && stage != RB_END) {
+                // material.sample (path or MIS): the coat's coin, then the base's lobe
+                if (stage == RB_PATH || stage == RB_MIS) {
+                    const bool mis = stage == RB_MIS;
+                    bool       done = false;
+                    MSample    r;
+                    if (coat && next1D(c.rng) < fc) {
+                        r    = coat_reflect(top, fc, wo_l);
+                        done = true;
+                    } else if (glossy) {
+                        need  = true;
+                        stage = mis ? RB_MIS_W : RB_PATH_W;
+                    } else {
+                        r = lambert_sample(base, c.rng);
+                        if (coat) r = coat_wrap(top, fc, r);
+                        done = true;
+                    }
+                    if (done) {
+                        if (mis) ms = r;
+                        else s = r;
+                        stage = mis ? RB_MIS_DONE : RB_PATH_DONE;
+                    }
+                } else if (stage == RB_PATH_W || stage == RB_MIS_W) {
+                    MSample r = onesample_sample_w(base, wo_l, w, c.rng, c.q);
+                    if (coat) r = coat_wrap(top, fc, r);
+                    if (stage == RB_MIS_W) {
+                        ms    = r;
+                        stage = RB_MIS_DONE;
+                    } else {
+                        s     = r;
+                        stage = RB_PATH_DONE;
+                    }
+                } else if (stage == RB_PATH_DONE) { // material_sample's world transform and the path test
+                    if (s.pdf == 0.0f || cblack(s.color)) {
+                        path_ok = false;
+                        stage   = RB_END;
+                    } else {
+                        s.dir   = to_world(onb_of_unit(nv), s.dir);
+                        path_ok = true;
+                        li      = 0;
+                        stage   = RB_LIGHT;
+                    }
+                } else if (stage == RB_LIGHT) { // estimate_direct_mis: light sample, shadow ray
+                    if (li >= sc.n_lights) {
+                        stage = RB_END;
+                        continue;
+                    }
+                    Lr = mkc(0, 0, 0);
+                    const Light& l = sc.lights[li];
+                    ls             = light_sample(sc, l, P, n, next2D(c.rng), c.q);
+                    if (ls.pdf == 0.0f || cblack(ls.L) || occluded(c, ls.ray, ls.tmin, ls.tmax)) {
+                        L = cadd(L, cmul(throughput, Lr));
+                        ++li;
+                        continue;
+                    }
+                    wi_l = to_onb(onb_of_unit(nv), ls.ray.d);
+                    lcos = abs_f(dot(ls.ray.d, n));
+                    if (glossy) {
+                        need  = true;
+                        stage = RB_EVAL_W;
+                    } else {
+                        const rgb be = coat ? cscale(lambert_eval(base), 1.0f - fc) : lambert_eval(base);
+                        eval_black   = cblack(be);
+                        beL          = cmul(be, ls.L);
+                        stage        = RB_EVAL_DONE;
+                    }
+                } else if (stage == RB_EVAL_W) {
+                    const rgb v  = onesample_eval_w(base, wo_l, wi_l, w, c.q);
+                    const rgb be = coat ? cscale(v, 1.0f - fc) : v;
+                    eval_black   = cblack(be);
+                    beL          = cmul(be, ls.L);
+                    stage        = RB_EVAL_DONE;
+                } else if (stage == RB_EVAL_DONE) { // material.pdf when the eval is not black
+                    if (eval_black) {
+                        stage = RB_MIS;
+                    } else if (glossy) {
+                        need  = true;
+                        stage = RB_PDF_W;
+                    } else {
+                        bp    = coat ? (1.0f - fc) * lambert_pdf(base) : lambert_pdf(base);
+                        stage = RB_PDF_DONE;
+                    }
+                } else if (stage == RB_PDF_W) {
+                    const float v = onesample_pdf_w(base, wo_l, wi_l, w, c.q);
+                    bp            = coat ? (1.0f - fc) * v : v;
+                    stage         = RB_PDF_DONE;
+                } else if (stage == RB_PDF_DONE) {
+                    if (bp > 0.0f) {
+                        const float wgt = balance(ls.pdf, ls.pdf + bp);
+                        Lr              = cadd(Lr, cscale(beL, lcos * wgt / ls.pdf));
+                    }
+                    stage = RB_MIS;
+                } else if (stage == RB_MIS_DONE) { // the MIS direction: light pdf, MIS ray
+                    if (!(ms.pdf == 0.0f || cblack(ms.color))) {
+                        ms.dir         = to_world(onb_of_unit(nv), ms.dir);
+                        const Light& l = sc.lights[li];
+                        const float  lp = light_pdf(sc, l, P, ms.dir);
+                        if (lp != 0.0f) {
+                            const float wgt = balance(ms.pdf, ms.pdf + lp);
+                            Ray         mr;
+                            mr.o             = P;
+                            mr.d             = ms.dir;
+                            const float mmin = ray_offset(n, ms.dir);
+                            ++c.rays;
+                            const LightHit lh = scene_intersect_lights(sc, mr, mmin, k_infinite, c.st);
+                            if (lh.hit) {
+                                if (!occluded(c, mr, mmin, k_infinite))
+                                    Lr = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, light_hit_L(sc, lh, mr.d, c.q)),
+                                                                      abs_f(dot(ms.dir, n))), wgt), ms.pdf));
+                            }
+                        }
+                    }
+                    L = cadd(L, cmul(throughput, Lr));
+                    ++li;
+                    stage = RB_LIGHT;
+                }
+            }
+            if (!__any(need)) break;
+            if (need) glossy_weights(base, wo_l, c.rng, c.q, w); // one copy for every call site
+        }
+        if (!path_ok) break;
+        const f3    wi     = s.dir;
+        const float cosine = abs_f(dot(wi, n));
+        throughput         = cmul(throughput, cdivs(cscale(s.color, cosine), s.pdf));
+        if (depth >= sc.rr_depth) {
+            const float lum = luminance(throughput);
+            if (lum < rr_cut) {
+                const float qv = std_max(0.05f, lum / rr_cut);
+                if (next1D(c.rng) < qv) throughput = cdivs(throughput, qv);
+                else break;
+            }
+        }
+        ray.o = next_o;
+        ray.d = wi;
+        tmin  = ray_offset(cosine);
+        tmax  = k_infinite;
     }
     return L;
 }
