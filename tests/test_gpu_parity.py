@@ -375,3 +375,4 @@ def test_rrnee_merged_estimates_bitexact(scene_dir, monkeypatch, scene, w, h, bv
         c, cst = _oracle.render(s, 5, 3, variant="spm")
         assert ast.rays == cst["rays"] and ast.shadow_rays == cst["shadow_rays"]
         assert np.array_equal(a.view(np.uint32), c.view(np.uint32)), rel_l2(a, c)
+
