@@ -64,6 +64,11 @@ struct RsqrtTable {
     int32_t         bits;
     uint32_t        zero_result;   // RSQRTSS(+0)
     uint32_t        denorm_result; // RSQRTSS(smallest positive denormal) -- class behaviour
+    // Packed form (device copies): pack_shift > 0 means `entries` holds 16-bit values v and the
+    // result bits are pack_hi | v << pack_shift (every captured table so far: one exponent, 12
+    // significant mantissa bits -- half the LDS of 32-bit entries).
+    int32_t  pack_shift = 0;
+    uint32_t pack_hi    = 0;
 };
 
 SP_HD float rsqrtss_emulated(float x, const RsqrtTable& t)
@@ -87,7 +92,8 @@ SP_HD float rsqrtss_emulated(float x, const RsqrtTable& t)
     const int32_t  p    = ex & 1;
     const int32_t  q    = (ex - p) / 2;
     const uint32_t m    = (u & 0x7fffffu) >> (23 - t.bits);
-    const uint32_t r    = t.entries[((uint32_t)p << t.bits) | m];
+    const uint32_t i    = ((uint32_t)p << t.bits) | m;
+    const uint32_t r    = t.pack_shift ? (t.pack_hi | ((uint32_t)((const uint16_t*)t.entries)[i] << t.pack_shift)) : t.entries[i];
     const int32_t  re   = (int32_t)((r >> 23) & 0xffu) - q;
     return u2f((r & 0x807fffffu) | ((uint32_t)re << 23));
 }

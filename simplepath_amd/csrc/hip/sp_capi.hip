@@ -760,8 +760,33 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
     d.envs = nullptr;
     up(envs, &d.envs);
     up(mats, &d.materials);
-    up(rc.entries, &d.rsqrt_entries);
+    // RSQRTSS table as 16-bit device entries when every entry has the same sign and exponent and
+    // at least 7 trailing zero mantissa bits (Intel and AMD hosts alike: exponent 126, 12
+    // significant bits): half the LDS each shading block copies it into (sp_math.h).
+    int      rs_shift = 23;
+    uint32_t rs_hi    = rc.entries[0] & 0xff800000u;
+    for (uint32_t e : rc.entries) {
+        if ((e & 0xff800000u) != rs_hi) {
+            rs_shift = 0;
+            break;
+        }
+        while (rs_shift > 0 && (e & ((1u << rs_shift) - 1u))) --rs_shift;
+    }
+    if (const char* v = std::getenv("SP_RSQRT_PACK")) // 0: 32-bit entries (comparison)
+        if (std::atoi(v) == 0) rs_shift = 0;
+    if (rs_shift < 7) rs_shift = 0;
+    if (rs_shift) {
+        std::vector<uint16_t> packed(rc.entries.size());
+        for (size_t i = 0; i < packed.size(); ++i) packed[i] = (uint16_t)((rc.entries[i] & 0x7fffffu) >> rs_shift);
+        const uint16_t* pk = nullptr;
+        up(packed, &pk);
+        d.rsqrt_entries = reinterpret_cast<const uint32_t*>(pk);
+    } else {
+        up(rc.entries, &d.rsqrt_entries);
+    }
     if (rc2 != SP_OK) return rc2;
+    d.rsqrt_shift  = rs_shift;
+    d.rsqrt_hi     = rs_shift ? rs_hi : 0u;
     d.rsqrt_bits   = rc.bits;
     d.rsqrt_zero   = rc.zero_result;
     d.rsqrt_denorm = rc.denorm_result;
@@ -1066,7 +1091,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // in parallel, and the in-order sum.  Chunks per pixel: enough work items to keep the
         // chip busy when the slowest pixel's chain would otherwise set the frame time (~120K
         // (tile, chunk) items was best on bunny's 2/4/8-way shards: tools/gpu_sweep_chunks.sh).
-        const int    rs_words  = 2 << s->dev.rsqrt_bits;
+        const int    rs_words  = spd::rsqrt_words(s->dev);
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         const uint32_t spp       = spp_u;
@@ -1144,7 +1169,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         ck_camera_rays = s->dev.max_depth > 0 ? (unsigned long long)inside * spp : 0ull;
         ck_samples     = (unsigned long long)inside * spp;
     } else {
-        const int    rs_words  = 2 << s->dev.rsqrt_bits;
+        const int    rs_words  = spd::rsqrt_words(s->dev);
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         int variant = 0;

@@ -47,11 +47,11 @@ struct Lds {
 __device__ __forceinline__ Lds lds_setup(const Scene& sc, uint32_t* lds, bool stack)
 {
     const int tid      = threadIdx.x;
-    const int rs_words = 2 << sc.rsqrt_bits;
+    const int rs_words = rsqrt_words(sc);
     for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
     __syncthreads();
-    Lds l{ Rsq{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm },
+    Lds l{ Rsq{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi },
            Stack{ lds + rs_words + (stack ? (tid >> 6) * sc.stack_words * 64 : 0), tid & 63, sc.stack_depth } };
     return l;
 }
@@ -404,7 +404,7 @@ int chunk_blocks_per_cu(size_t lds_bytes)
 
 hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int eval_waves, hipStream_t stream)
 {
-    const size_t rs_bytes    = (size_t)(2 << sc.rsqrt_bits) * 4;
+    const size_t rs_bytes    = (size_t)rsqrt_words(sc) * 4;
     const size_t stack_bytes = (size_t)WAVES_PER_BLOCK * sc.stack_words * 64 * 4;
     const int64_t cam_waves  = a.num_tiles * (int64_t)a.spp;
     hipLaunchKernelGGL(ck_camera, dim3((unsigned)((cam_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),

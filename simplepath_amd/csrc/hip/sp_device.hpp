@@ -104,9 +104,11 @@ struct Scene {
 
     const Material* materials;
 
-    const uint32_t* rsqrt_entries; // 2 << rsqrt_bits
+    const uint32_t* rsqrt_entries; // 2 << rsqrt_bits entries; 16-bit when rsqrt_shift > 0 (sp_math.h)
     int32_t         rsqrt_bits;
     uint32_t        rsqrt_zero, rsqrt_denorm;
+    int32_t         rsqrt_shift;
+    uint32_t        rsqrt_hi;
     int             stack_depth;   // LDS traversal stack entries per lane (0 when stackless)
     int             stack_words;   // LDS words per lane
     int             ordered;       // 1: SAH BVH -- visit the near child (split axis, ray sign) first
@@ -116,6 +118,9 @@ struct Scene {
     const uint32_t* parents;       // parent of each geometry node (root: itself)
     const uint32_t* light_parents; // parent of each light-BVH node
 };
+// 32-bit words of the RSQRTSS table (the LDS copy every shading kernel makes)
+__host__ __device__ inline int rsqrt_words(const Scene& sc) { return sc.rsqrt_shift ? (1 << sc.rsqrt_bits) : (2 << sc.rsqrt_bits); }
+
 
 struct RenderArgs {
     float*          out;        // tile-packed radiance

@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(256) tile_cost_kernel(Scene sc, const int32_t*
     const uint32_t lane = threadIdx.x & 63u;
     if (slot >= n_tiles) return;
     const Stack    st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, (int)lane, sc.stack_depth };
-    const Rsq      q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+    const Rsq      q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
     const int32_t  tile = tile_ids ? tile_ids[slot] : (int32_t)slot;
     const uint32_t px   = (uint32_t)((tile % tiles_x) * 8) + morton_decode_1(lane);
     const uint32_t py   = (uint32_t)((tile / tiles_x) * 8) + morton_decode_1(lane >> 1);

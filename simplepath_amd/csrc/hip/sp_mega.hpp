@@ -35,11 +35,11 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
     const int tid  = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int rs_words = 2 << sc.rsqrt_bits;
+    const int rs_words = rsqrt_words(sc);
     for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
     __syncthreads();
-    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
     Stack st{ lds + rs_words + wave * sc.stack_words * 64, lane, sc.stack_depth };
 
     const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;
@@ -182,11 +182,11 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_regen(Sc
     const int tid  = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int rs_words = 2 << sc.rsqrt_bits;
+    const int rs_words = rsqrt_words(sc);
     for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
     __syncthreads();
-    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
     Stack st{ lds + rs_words + wave * sc.stack_words * 64, lane, sc.stack_depth };
 
     const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;

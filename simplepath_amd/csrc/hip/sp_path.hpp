@@ -24,11 +24,13 @@ struct Rsq {
     const uint32_t* t;
     int32_t         bits;
     uint32_t        zero, denorm;
+    int32_t         shift; // 16-bit entries when > 0 (RsqrtTable::pack_shift)
+    uint32_t        hi;
 };
 
 __device__ __forceinline__ float rsqrt_ref(float a, const Rsq& q)
 {
-    RsqrtTable tb{ q.t, q.bits, q.zero, q.denorm };
+    RsqrtTable tb{ q.t, q.bits, q.zero, q.denorm, q.shift, q.hi };
     return rsqrt_newton(a, rsqrtss_emulated(a, tb));
 }
 __device__ __forceinline__ f3 normalize(f3 a, const Rsq& q) { return scale(a, rsqrt_ref(dot(a, a), q)); }

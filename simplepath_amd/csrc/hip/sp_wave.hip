@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_PRIM_WAVES) wf_primary(Scene sc, 
     float4         hrec = make_float4(0.0f, __uint_as_float(0xffffffffu), 0.0f, 0.0f);
     uint32_t       rays = 0, hits = 0;
     if (pr.inside && sc.max_depth > 0) {
-        const Rsq   q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+        const Rsq   q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
         const Ray   ray  = camera_ray(sc, pr, sample, q);
         float       tmax = k_infinite;
         const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
@@ -214,7 +214,7 @@ template <int MINW>
 __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w, uint32_t sample)
 {
     extern __shared__ uint32_t lds[];
-    const int rs_words = 2 << sc.rsqrt_bits;
+    const int rs_words = rsqrt_words(sc);
     for (int i = threadIdx.x; i < rs_words; i += WF_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(threadIdx.x, WF_BLOCK);
     __syncthreads();
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
 #define SP_STAMP(k) ((void)0)
 #endif
     if (pr.inside) {
-        const Rsq q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+        const Rsq q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
         Rng       rng = rng_load(w, p);
         rng_prepare(rng);
         SP_STAMP(1);
@@ -454,7 +454,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
         if (ev) (void)hipEventRecord(ev[e++], stream);
     };
     const size_t stack_lds = (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
-    const size_t rs_lds    = (size_t)(2 << sc.rsqrt_bits) * 4;
+    const size_t rs_lds    = (size_t)rsqrt_words(sc) * 4;
     const unsigned grid_all = (unsigned)((w.n + WF_BLOCK - 1) / WF_BLOCK);
 
     // Parts: tile sets with their own queues, each driven by its own stream, so that one part's

@@ -200,7 +200,7 @@ __device__ void slot_begin(const Scene& sc, const PathArgs& a, int32_t slot, int
 __global__ void __launch_bounds__(WP_BLOCK) wp_init(Scene sc, PathArgs a)
 {
     extern __shared__ uint32_t lds[];
-    const Rsq     q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+    const Rsq     q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
     const int32_t slot = (int32_t)((blockIdx.x * WP_BLOCK + threadIdx.x) >> 6);
     if (slot >= a.slots) return;
     const int32_t pos = slot < a.num_tiles ? slot : -1;
@@ -455,7 +455,7 @@ template <int INTEG, int MINW>
 __global__ void __launch_bounds__(WP_BLOCK, MINW) wp_shade(Scene sc, PathArgs a)
 {
     extern __shared__ uint32_t lds[];
-    const int rs_words = 2 << sc.rsqrt_bits;
+    const int rs_words = rsqrt_words(sc);
     for (int i = threadIdx.x; i < rs_words; i += WP_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(threadIdx.x, WP_BLOCK);
     __syncthreads();
@@ -463,7 +463,7 @@ __global__ void __launch_bounds__(WP_BLOCK, MINW) wp_shade(Scene sc, PathArgs a)
     if (slot >= a.slots) return;
     const int32_t pos = a.slot_tile[slot];
     if (pos < 0) return;
-    const Rsq      q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm };
+    const Rsq      q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t  p    = (int64_t)slot * 64 + lane;
     const Pix      pr   = pixel_of(sc, a, pos, lane);
@@ -575,7 +575,7 @@ hipError_t wpath_render(const Scene& sc, const WPathRun& r, hipStream_t stream, 
     if ((e = hipMemsetAsync(a.wstat, 0, (size_t)a.slots * ST_N * 8, stream)) != hipSuccess) return e;
     const unsigned grid      = (unsigned)((a.slots + (WP_BLOCK / 64) - 1) / (WP_BLOCK / 64));
     const size_t   stack_lds = (size_t)(WP_BLOCK / 64) * sc.stack_words * 64 * 4;
-    const size_t   rs_lds    = (size_t)(2 << sc.rsqrt_bits) * 4;
+    const size_t   rs_lds    = (size_t)rsqrt_words(sc) * 4;
     hipLaunchKernelGGL(wp_init, dim3(grid), dim3(WP_BLOCK), 0, stream, sc, a);
     // (trace, shade) rounds until no slot holds a tile.  The active count is copied to host
     // memory after every WP_POLL rounds and read one batch later (no stall in the loop).
