@@ -1148,6 +1148,7 @@ __device__ __forceinline__ P2 beckmann_sample11(float cos_theta_i, float U1, flo
     const float sqrt_pi_inv = 1.0f / sqrt_f(k_pi);
     const float normalization =
         1.0f / (1.0f + c + sqrt_pi_inv * tan_theta_i * lm_expf(-cot_theta_i * cot_theta_i));
+#pragma unroll 1 // data-dependent exit: unrolled copies only grow the hot loop
     for (int it = 0; it < 9; ++it) {
         if (!(b >= a && b <= c)) b = 0.5f * (a + c);
         const float inv_erf = erfinv(b);
@@ -1308,6 +1309,7 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     // the final erfinv is only evaluated when the loop ran out of iterations (b moved after it)
     float inv_erf   = 0.0f;
     bool  converged = false;
+#pragma unroll 1 // data-dependent exit: unrolled copies only grow the hot loop
     for (int it = 0; it < 9; ++it) {
         if (!(b >= a && b <= c)) b = 0.5f * (a + c);
         inv_erf = erfinv(b);
@@ -1523,22 +1525,30 @@ __device__ __forceinline__ float onesample_pdf(const Material& m, f3 wo, f3 wi, 
 }
 
 // Material::sample/eval/pdf incl. ClearcoatMaterial (materials/Material.h:461-529, 723-806)
+// A clearcoat's base and a plain material share ONE inlined copy of the OneSample code (the
+// 16-sample glossy estimate is ~5 K instructions): the coat only selects which record that copy
+// reads and wraps its result.  Two copies measured as two hot loops competing for the
+// instruction cache.  The coat's Fresnel term draws nothing, so computing it before or after the
+// base changes no value.
 __device__ __forceinline__ MSample material_sample_local(const Scene& sc, int mid, f3 wo, Rng& rng, const Rsq& q)
 {
-    const Material& m = sc.materials[mid];
-    if (m.kind != SP_MAT_CLEARCOAT) return onesample_sample(m, wo, rng, q);
-    const float f = fresnel_dielectric(wo.y, 1.0f, m.coat_ior);
-    const float u = next1D(rng);
-    if (u < f) {
-        MSample s;
-        s.dir   = mk(-wo.x, wo.y, -wo.z);
-        s.color = cdivs(cscale(m.coat_color, f), abs_f(s.dir.y));
-        s.pdf   = f;
-        s.props = PROP_SPECULAR | PROP_REFLECTIVE;
-        return s;
+    const Material& m    = sc.materials[mid];
+    const bool      coat = m.kind == SP_MAT_CLEARCOAT;
+    float           f    = 0.0f;
+    if (coat) {
+        f             = fresnel_dielectric(wo.y, 1.0f, m.coat_ior);
+        const float u = next1D(rng);
+        if (u < f) {
+            MSample s;
+            s.dir   = mk(-wo.x, wo.y, -wo.z);
+            s.color = cdivs(cscale(m.coat_color, f), abs_f(s.dir.y));
+            s.pdf   = f;
+            s.props = PROP_SPECULAR | PROP_REFLECTIVE;
+            return s;
+        }
     }
-    MSample b = onesample_sample(sc.materials[m.base], wo, rng, q);
-    if (b.pdf == 0.0f) return b;
+    const MSample b = onesample_sample(sc.materials[coat ? m.base : mid], wo, rng, q);
+    if (!coat || b.pdf == 0.0f) return b;
     MSample s;
     s.pdf   = (1.0f - f) * b.pdf;
     s.color = cmul(csub(mkc(1, 1, 1), cscale(m.coat_color, f)), b.color);
@@ -1548,17 +1558,21 @@ __device__ __forceinline__ MSample material_sample_local(const Scene& sc, int mi
 }
 __device__ __forceinline__ rgb material_eval_local(const Scene& sc, int mid, f3 wo, f3 wi, Rng& rng, const Rsq& q)
 {
-    const Material& m = sc.materials[mid];
-    if (m.kind != SP_MAT_CLEARCOAT) return onesample_eval(m, wo, wi, rng, q);
+    const Material& m    = sc.materials[mid];
+    const bool      coat = m.kind == SP_MAT_CLEARCOAT;
+    const rgb       r    = onesample_eval(sc.materials[coat ? m.base : mid], wo, wi, rng, q);
+    if (!coat) return r;
     const float f = fresnel_dielectric(wo.y, 1.0f, m.coat_ior);
-    return cscale(onesample_eval(sc.materials[m.base], wo, wi, rng, q), 1.0f - f);
+    return cscale(r, 1.0f - f);
 }
 __device__ __forceinline__ float material_pdf_local(const Scene& sc, int mid, f3 wo, f3 wi, Rng& rng, const Rsq& q)
 {
-    const Material& m = sc.materials[mid];
-    if (m.kind != SP_MAT_CLEARCOAT) return onesample_pdf(m, wo, wi, rng, q);
+    const Material& m    = sc.materials[mid];
+    const bool      coat = m.kind == SP_MAT_CLEARCOAT;
+    const float     p    = onesample_pdf(sc.materials[coat ? m.base : mid], wo, wi, rng, q);
+    if (!coat) return p;
     const float f = fresnel_dielectric(wo.y, 1.0f, m.coat_ior);
-    return (1.0f - f) * onesample_pdf(sc.materials[m.base], wo, wi, rng, q);
+    return (1.0f - f) * p;
 }
 
 __device__ __forceinline__ MSample material_sample(const Scene& sc, int mid, f3 wo_w, f3 n, Rng& rng, const Rsq& q)
