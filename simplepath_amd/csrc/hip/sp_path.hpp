@@ -165,6 +165,24 @@ __device__ __forceinline__ void rng_skip(Rng& r, int n)
     r.pfn = 0;
 }
 
+// Pull the next n words of this lane's stream toward the CU before they are drawn.  The state
+// (2.5 KB per pixel, gigabytes per frame) was written many kernels ago and lives in HBM, so each
+// draw of a 32-draw glossy estimate would otherwise wait one full memory latency.  The words are
+// fetched with LDS-DMA loads into a sink that nobody reads: no VGPR is held, all n are in flight
+// at once, and the draws that follow hit L2.  Only the cache state changes -- the stream, the
+// buffers and every value drawn are exactly as without it.  Rows past the current generation are
+// touched in the next buffer only when it already holds the next generation.
+__device__ __forceinline__ void rng_touch(const Rng& r, int n, __attribute__((address_space(3))) void* sink)
+{
+    const uint64_t* cur  = r.base + (size_t)r.cur * MT_N * 64;
+    const uint64_t* next = r.base + (size_t)mt_next(r) * MT_N * 64;
+    for (int k = 0; k < n; ++k) {
+        const int row = r.idx + k;
+        if (row < MT_N) __builtin_amdgcn_global_load_lds((const void*)(cur + (size_t)row * 64), sink, 4, 0, 0);
+        else if (r.ready) __builtin_amdgcn_global_load_lds((const void*)(next + (size_t)(row - MT_N) * 64), sink, 4, 0, 0);
+    }
+}
+
 // IncoherentSampler::get_next_1D / get_next_2D (math/Sampler.h:110-118)
 __device__ __forceinline__ float next1D(Rng& r) { return canonical_from_u64(rng_raw(r)); }
 struct P2 {
@@ -1525,6 +1543,14 @@ __device__ __forceinline__ float onesample_pdf(const Material& m, f3 wo, f3 wi, 
 }
 
 // Material::sample/eval/pdf incl. ClearcoatMaterial (materials/Material.h:461-529, 723-806)
+// Does Material::eval / sample / pdf at this record run the 16-sample glossy estimate?
+__device__ __forceinline__ bool material_has_rho(const Scene& sc, int mid)
+{
+    const Material& m = sc.materials[mid];
+    const int       k = (m.kind == SP_MAT_CLEARCOAT) ? sc.materials[m.base].kind : m.kind;
+    return k == SP_MAT_GLOSSY;
+}
+
 // A clearcoat's base and a plain material share ONE inlined copy of the OneSample code (the
 // 16-sample glossy estimate is ~5 K instructions): the coat only selects which record that copy
 // reads and wraps its result.  Two copies measured as two hot loops competing for the

@@ -32,6 +32,10 @@
 #define SP_WAVE_RNG_PF 0
 #endif
 #define SP_RNG_PF SP_WAVE_RNG_PF
+// Rows of the RNG stream wf_shade pulls into L2 ahead of a glossy hit's draws (rng_touch; 0 = off).
+#ifndef SP_WAVE_RNG_TOUCH
+#define SP_WAVE_RNG_TOUCH 68
+#endif
 #include "sp_path.hpp"
 #include "sp_wave.hpp"
 
@@ -214,6 +218,10 @@ template <int MINW>
 __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w, uint32_t sample)
 {
     extern __shared__ uint32_t lds[];
+#if SP_WAVE_RNG_TOUCH
+    __shared__ uint32_t rng_sink_words[64]; // LDS-DMA target of rng_touch, never read
+    auto* rng_sink = (__attribute__((address_space(3))) void*)rng_sink_words;
+#endif
     const int rs_words = rsqrt_words(sc);
     for (int i = threadIdx.x; i < rs_words; i += WF_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(threadIdx.x, WF_BLOCK);
@@ -245,6 +253,10 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
             const Ray   ray = camera_ray(sc, pr, sample, q);
             const Isect is  = finish_hit(sc, h, ray, q);
             const f3    wo  = neg(ray.d);
+#if SP_WAVE_RNG_TOUCH
+            // a glossy hit draws 2 + 32 words per light (light sample, 16-sample rho estimate)
+            if (material_has_rho(sc, is.material)) rng_touch(rng, std::min(34 * sc.n_lights, SP_WAVE_RNG_TOUCH), rng_sink);
+#endif
             SP_STAMP(2);
             for (int li = 0; li < sc.n_lights; ++li) {
                 const Light   l  = uload_light(sc.lights + li);
