@@ -261,6 +261,10 @@ SP_HD double sincosf_reduce_large(uint32_t xi, int* np)
     return x * u2d(glibc::PI63[0]);
 }
 
+// BOUNDED: the caller guarantees a finite |y| < 120 (abstop <= 0x42e), e.g. 2*pi*u for a canonical
+// u in [0, 1).  Such inputs take one of the first two paths of the full function, so leaving the
+// large-argument reduction (and its registers) out of the code changes no result.
+template <bool BOUNDED = false>
 SP_HD float lm_sinf(float y)
 {
     const uint32_t iy     = f2u(y);
@@ -271,7 +275,7 @@ SP_HD float lm_sinf(float y)
         if (abstop <= 0x397u) return y;
         return sincosf_poly(x, s, 0, 0);
     }
-    if (abstop <= 0x42eu) {
+    if (BOUNDED || abstop <= 0x42eu) {
         const double r  = x * sc(0, SC_HPI_INV);
         int          n  = (((int32_t)r) + 0x800000) >> 24;
         x               = dfma(-(double)n, sc(0, SC_HPI), x);
@@ -291,6 +295,7 @@ SP_HD float lm_sinf(float y)
     return ((iy & 0x7fffffffu) > 0x7f800000u) ? x86_quiet(y) : x86_default_nan();
 }
 
+template <bool BOUNDED = false> // as lm_sinf
 SP_HD float lm_cosf(float y)
 {
     const uint32_t iy     = f2u(y);
@@ -301,7 +306,7 @@ SP_HD float lm_cosf(float y)
         if (abstop <= 0x397u) return 1.0f;
         return sincosf_poly(x, s, 0, 1);
     }
-    if (abstop <= 0x42eu) {
+    if (BOUNDED || abstop <= 0x42eu) {
         const double r  = x * sc(0, SC_HPI_INV);
         int          n  = (((int32_t)r) + 0x800000) >> 24;
         x               = dfma(-(double)n, sc(0, SC_HPI), x);

@@ -810,7 +810,8 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
         if (rc2 != SP_OK) return rc2;
         d.stack_depth = 0;
     }
-    d.stack_words = d.stack_depth;
+    d.stack_words     = d.stack_depth;
+    d.any_stack_words = d.stackless ? 0 : std::max(wide.words.empty() ? bvh.max_depth : wide.depth, lbvh.max_depth) + 1;
     SP_HIP(hipMalloc(&s->tile_counter, sizeof(int32_t)));
     SP_HIP(hipMalloc(&s->counters, 8 * sizeof(unsigned long long)));
     SP_HIP(hipEventCreate(&s->ev0));

@@ -111,6 +111,9 @@ struct Scene {
     uint32_t        rsqrt_hi;
     int             stack_depth;   // LDS traversal stack entries per lane (0 when stackless)
     int             stack_words;   // LDS words per lane
+    // any-hit-only kernels (wf_shadow): their walks need max(wide or binary depth, light depth) + 1
+    // stack entries, usually far fewer than stack_words (which covers the binary closest-hit walk)
+    int             any_stack_words;
     int             ordered;       // 1: SAH BVH -- visit the near child (split axis, ray sign) first
     // BVHs too deep for the LDS stack budget: binary walks climb parent links instead of popping
     // a stack (same visiting order and box tests; sp_path.hpp bvh_next)

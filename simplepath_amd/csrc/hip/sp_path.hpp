@@ -115,10 +115,13 @@ __device__ __forceinline__ void rng_prepare(Rng& r)
     }
 }
 
+// NT ("no twist"): the caller has made sure the next generation is ready (rng_reserve), so the
+// twist is not inlined at this draw -- its code and registers stay out of hot loops.
+template <bool NT = false>
 __device__ __forceinline__ uint64_t rng_raw(Rng& r)
 {
     if (r.idx >= MT_N) {
-        if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+        if (!NT && !r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
         r.cur   = mt_next(r);
         r.idx   = 0;
         r.ready = r.pre;
@@ -183,8 +186,20 @@ __device__ __forceinline__ void rng_touch(const Rng& r, int n, __attribute__((ad
     }
 }
 
+// Make the next n draws twist-free: if they run past the current generation and the next one is
+// not there yet, twist it now.  A twist reads only the current generation, so computing it before
+// its first word is drawn gives the same words as twisting at the boundary.
+__device__ __forceinline__ void rng_reserve(Rng& r, int n)
+{
+    if (!r.ready && r.idx + n > MT_N) {
+        mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+        r.ready = 1;
+    }
+}
+
 // IncoherentSampler::get_next_1D / get_next_2D (math/Sampler.h:110-118)
-__device__ __forceinline__ float next1D(Rng& r) { return canonical_from_u64(rng_raw(r)); }
+template <bool NT = false>
+__device__ __forceinline__ float next1D(Rng& r) { return canonical_from_u64(rng_raw<NT>(r)); }
 struct P2 {
     float x, y;
 };
@@ -1013,7 +1028,7 @@ __device__ __forceinline__ f3 sample_uniform_sphere(P2 u)
     const float z   = 1.0f - 2.0f * u.x;
     const float r   = sqrt_f(std_max(0.0f, 1.0f - z * z));
     const float phi = (float)(2.0 * (double)k_pi * (double)u.y);
-    return mk(r * lm_cosf(phi), r * lm_sinf(phi), z);
+    return mk(r * lm_cosf<true>(phi), r * lm_sinf<true>(phi), z); // u in [0, 1): |phi| < 2 pi
 }
 // math/Sampling.h:235
 __device__ __forceinline__ f3 sample_uniform_hemisphere(P2 u)
@@ -1021,7 +1036,7 @@ __device__ __forceinline__ f3 sample_uniform_hemisphere(P2 u)
     const float y   = u.x;
     const float r   = sqrt_f(std_max(0.0f, 1.0f - y * y));
     const float phi = 2.0f * k_pi * u.y;
-    return mk(r * lm_cosf(phi), y, r * lm_sinf(phi));
+    return mk(r * lm_cosf<true>(phi), y, r * lm_sinf<true>(phi)); // u in [0, 1): |phi| < 2 pi
 }
 // math/Sampling.cpp:304
 __device__ __forceinline__ P2 concentric_disk(P2 u)
@@ -1035,8 +1050,8 @@ __device__ __forceinline__ P2 concentric_disk(P2 u)
     float theta, rad;
     if (abs_f(ox) > abs_f(oy)) { rad = ox; theta = pi_over_4 * (oy / ox); }
     else { rad = oy; theta = pi_over_2 - pi_over_4 * (ox / oy); }
-    r.x = rad * lm_cosf(theta);
-    r.y = rad * lm_sinf(theta);
+    r.x = rad * lm_cosf<true>(theta); // |theta| <= 3 pi / 4
+    r.y = rad * lm_sinf<true>(theta);
     return r;
 }
 __device__ __forceinline__ f3 sample_cosine_hemisphere(P2 u)
@@ -1148,8 +1163,8 @@ __device__ __forceinline__ P2 beckmann_sample11(float cos_theta_i, float U1, flo
     P2 s;
     if (cos_theta_i > .9999f) {
         const float r  = sqrt_f(-lm_logf(1.0f - U1));
-        const float sp = lm_sinf(2.0f * k_pi * U2);
-        const float cp = lm_cosf(2.0f * k_pi * U2);
+        const float sp = lm_sinf<true>(2.0f * k_pi * U2); // U2 in [0, 1): bounded argument
+        const float cp = lm_cosf<true>(2.0f * k_pi * U2);
         s.x = r * cp;
         s.y = r * sp;
         return s;
@@ -1313,8 +1328,8 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     P2 s;
     if (p.steep) {
         const float r  = sqrt_f(-lm_logf(1.0f - U1));
-        const float sp = lm_sinf(2.0f * k_pi * U2);
-        const float cp = lm_cosf(2.0f * k_pi * U2);
+        const float sp = lm_sinf<true>(2.0f * k_pi * U2); // U2 in [0, 1): bounded argument
+        const float cp = lm_cosf<true>(2.0f * k_pi * U2);
         s.x = r * cp;
         s.y = r * sp;
         return s;
@@ -1347,6 +1362,7 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     return s;
 }
 // mf_sample with the precomputed wo terms (draw order: U2, then U1)
+template <bool NT = false>
 __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPre& p, f3 wo, Rng& rng, const Rsq& q)
 {
     MSample r;
@@ -1355,8 +1371,8 @@ __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPr
     r.pdf   = 0.0f;
     r.props = 0;
     if (wo.y == 0.0f) return r;
-    const float U2 = next1D(rng);
-    const float U1 = next1D(rng);
+    const float U2 = next1D<NT>(rng);
+    const float U1 = next1D<NT>(rng);
     P2          sl = beckmann_sample11_pre(p, U1, U2);
     const float tmp = p.cphi * sl.x - p.sphi * sl.y;
     sl.y            = p.sphi * sl.x + p.cphi * sl.y;
@@ -1398,8 +1414,9 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
 {
     const BeckPre p = beck_pre(m, wo, q);
     rgb           r = mkc(0, 0, 0);
+    rng_reserve(rng, 32); // the loop below draws at most 32 words and never twists
     for (unsigned i = 0; i < 16u; ++i) {
-        const MSample s = mf_sample_pre(m, p, wo, rng, q);
+        const MSample s = mf_sample_pre<true>(m, p, wo, rng, q);
         if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
     }
     return cdivs(r, (float)16u);

@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_TRAV_WAVES) wf_shadow(Scene sc, W
 {
     extern __shared__ uint32_t lds[];
     const int      lane  = threadIdx.x & 63;
-    const Stack    st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
+    const Stack    st{ lds + (threadIdx.x >> 6) * sc.any_stack_words * 64, lane, sc.any_stack_words };
     // Segment j holds the shadow pixels of tile slots j, j + QSEG, ... in arrival order.  Virtual
     // chunk v = 64 entries of segment v % QSEG starting at (v / QSEG) * 64: walking v in order
     // visits the tiles roughly in image order, which keeps neighbouring waves' BVH nodes in cache.
@@ -425,6 +425,8 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_stats(WaveArgs w, int64_t n_slots
 }
 
 // ---------------------------------------------------------------------------- host side
+// wf_shadow's LDS: per-wave any-hit stacks (wide-BVH depth, not the binary closest-hit depth)
+static size_t wave_shadow_lds(const Scene& sc) { return (size_t)(WF_BLOCK / 64) * sc.any_stack_words * 64 * 4; }
 static int shade_waves_env()
 {
     const char* v = std::getenv("SP_SHADE_WAVES");
@@ -465,8 +467,9 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     auto mark = [&]() {
         if (ev) (void)hipEventRecord(ev[e++], stream);
     };
-    const size_t stack_lds = (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
-    const size_t rs_lds    = (size_t)rsqrt_words(sc) * 4;
+    const size_t stack_lds  = (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
+    const size_t shadow_lds = wave_shadow_lds(sc);
+    const size_t rs_lds     = (size_t)rsqrt_words(sc) * 4;
     const unsigned grid_all = (unsigned)((w.n + WF_BLOCK - 1) / WF_BLOCK);
 
     // Parts: tile sets with their own queues, each driven by its own stream, so that one part's
@@ -548,7 +551,7 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
 #endif
             if (parts > 1) (void)hipEventRecord(shade_done[k], st);
             if (k == 0) mark();
-            hipLaunchKernelGGL(wf_shadow, dim3(sgrid[k]), dim3(WF_BLOCK), stack_lds, st, sc, wi);
+            hipLaunchKernelGGL(wf_shadow, dim3(sgrid[k]), dim3(WF_BLOCK), shadow_lds, st, sc, wi);
             hipLaunchKernelGGL(wf_accum, dim3(grid[k]), dim3(WF_BLOCK), 0, st, sc, wi);
             if (k == 0) mark();
         }
@@ -566,9 +569,8 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
 
 int wave_traverse_blocks_per_cu(const Scene& sc)
 {
-    const size_t stack_lds = (size_t)(WF_BLOCK / 64) * sc.stack_words * 64 * 4;
-    int          n         = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shadow, WF_BLOCK, stack_lds) != hipSuccess) return 1;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wf_shadow, WF_BLOCK, wave_shadow_lds(sc)) != hipSuccess) return 1;
     return n > 0 ? n : 1;
 }
 
