@@ -363,7 +363,8 @@ def roofline_of(stats, pixels, args, kernel_ms):
         achieved = alg / (kernel_ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "sp_render_kernel",
-                "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg}
+                "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg,
+                "valu": valu_of(args, "sp_render_kernel")}
     names = ["wf_init+wf_resolve", "wf_primary", "wf_shade", "wf_shadow"]
     tot = [sum(s.stage_ms[k] for s in stats) / n for k in range(4)]
     spp = args.spp

@@ -897,7 +897,11 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     // Below SP_CHUNK_MAX_TILES (default 12000: between the 2- and 4-GPU shards) even the
     // megakernel waits on single pixels' sample chains; the sample-chunk pipeline splits them
     // (4-GPU shard 1285 -> 1490, 8-GPU shard 823 -> 1384 Mrays/s).
-    int64_t wave_min = 24000, chunk_max = 12000;
+    // Round 2, device code without SLP vectorisation (profiles/r02/s5): the megakernel at 4 waves per
+    // SIMD renders the 1-GPU frame at 2706 Mrays/s against 2305 for the wavefront, and the sample
+    // chunks the 2-way shard at 2507 against 2138: AUTO now uses the wavefront only from
+    // SP_WAVE_MIN_TILES (default: never) and the chunks below SP_CHUNK_MAX_TILES = 24000.
+    int64_t wave_min = INT64_MAX, chunk_max = 24000;
     if (const char* v = std::getenv("SP_WAVE_MIN_TILES")) wave_min = std::atoll(v);
     if (const char* v = std::getenv("SP_CHUNK_MAX_TILES")) chunk_max = std::atoll(v);
     // sample-chunk buffers: per-sample hit records and radiance, the generator store (a
@@ -916,9 +920,15 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                                  (double)n_tiles * ck_gens * spm::MT_N * 64 * 8 + (double)ck_chunks * n_tiles * 64 * 4;
     double ck_max_gb = 96.0;
     if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) ck_max_gb = std::atof(v);
+    // with an image light ck_count replays Light::sample (draw counts depend on the drawn texel):
+    // the chunks then pay off only on smaller shards (spheres 1024^2 @ 64 spp, 16384 tiles: chunks
+    // 2902, megakernel 2973 Mrays/s)
+    bool image_light = false;
+    for (const auto& l : s->host->lights) image_light = image_light || l.kind == SP_LIGHT_IMAGE_ENVIRONMENT;
     if (pipeline == SP_PIPELINE_AUTO) {
         if (wave_ok && n_tiles >= wave_min) pipeline = SP_PIPELINE_WAVEFRONT;
-        else if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && n_tiles < chunk_max && ck_base_bytes <= ck_max_gb * 1e9)
+        else if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && n_tiles < (image_light ? chunk_max / 2 : chunk_max) &&
+                 ck_base_bytes <= ck_max_gb * 1e9)
             pipeline = SP_PIPELINE_SAMPLE_CHUNKS;
         else pipeline = SP_PIPELINE_MEGAKERNEL; // also when the chunk buffers would not fit the budget
     }
@@ -1173,7 +1183,14 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         const int    rs_words  = spd::rsqrt_words(s->dev);
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
-        int variant = 0;
+        // waves per SIMD the kernel is compiled for (SP_KERNEL_VARIANT): DirectLighting 4,
+        // IterativeRRNEE 3 -- but never more than the LDS lets run (one 4-wave block per wave per
+        // SIMD): a deep BVH's stacks (lucy: 3 blocks per CU) would leave the extra occupancy's
+        // register budget paid for in spills and unused (lucy 1080p @ 256 spp: 2007 Mrays/s at 3
+        // waves, 1879 at 4; profiles/r02/s5)
+        const int lds_waves = (int)std::min<size_t>(8, (160 * 1024) / lds_bytes);
+        int       variant   = integ == SP_INTEGRATOR_ITERATIVE_RRNEE ? 3 : 4;
+        variant             = std::max(2, std::min(variant, lds_waves));
         if (const char* v = std::getenv("SP_KERNEL_VARIANT")) variant = std::atoi(v);
         const int     per_cu  = spd::render_blocks_per_cu(integ, variant, lds_bytes);
         const int64_t max_blk = (int64_t)s->n_cu * per_cu;

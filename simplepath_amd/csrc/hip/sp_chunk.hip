@@ -30,6 +30,8 @@
 #endif
 #define SP_RNG_PF SP_CHUNK_RNG_PF
 #include "sp_chunk.hpp"
+
+#include <cstdlib>
 #include "sp_mega.hpp"
 
 namespace spd {
@@ -211,7 +213,8 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
 }
 
 // ------------------------------------------------------------------------- chunked shading
-__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_shade(Scene sc, ChunkArgs a)
+template <int MINW>
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) ck_shade(Scene sc, ChunkArgs a)
 {
     extern __shared__ uint32_t lds[];
     const Lds      l     = lds_setup(sc, lds, true);
@@ -395,10 +398,26 @@ __global__ void __launch_bounds__(256) ck_sum(Scene sc, ChunkArgs a)
     a.out[(size_t)p * 3 + 2] = acc.b;
 }
 
+// ck_shade occupancy request (SP_CK_WAVES, waves per SIMD): default 4 (128 VGPRs, ~210 B spill);
+// 2 = the compiler's choice (192 VGPRs, no spill), 3 = 168 VGPRs.  Bunny 8-way shard per GPU:
+// 1686 / 2039 / 2161 Mrays/s at 2 / 3 / 4 waves (profiles/r02/s5): the chunk kernel's lanes wait
+// on generator-store loads, and more waves hide them better than fewer spills do.
+typedef void (*CkShadeFn)(Scene, ChunkArgs);
+static CkShadeFn shade_kernel()
+{
+    const char* v = std::getenv("SP_CK_WAVES");
+    switch (v ? std::atoi(v) : 4) {
+    case 2: return ck_shade<1>;
+    case 3: return ck_shade<3>;
+    case 5: return ck_shade<5>;
+    default: return ck_shade<4>;
+    }
+}
+
 int chunk_blocks_per_cu(size_t lds_bytes)
 {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ck_shade, 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, shade_kernel(), 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess) return 1;
     return n > 0 ? n : 1;
 }
 
@@ -421,7 +440,7 @@ hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_bloc
         hipLaunchKernelGGL(ck_occl, dim3((unsigned)((cam_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
                            dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes, stream, sc, a);
     } else {
-        hipLaunchKernelGGL(ck_shade, dim3((unsigned)persistent_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes,
+        hipLaunchKernelGGL(shade_kernel(), dim3((unsigned)persistent_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes,
                            stream, sc, a);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -15,16 +15,17 @@ static bool regen_env()
     return v ? std::atoi(v) != 0 : false;
 }
 
-// The lock-step IterativeRRNEE megakernel runs with the selection-weight estimates merged across
-// call sites (sp_path.hpp integrate_rrnee_merged; identical images): 440 vs 395 Mrays/s on elf
-// 1024^2 x 16 spp.  SP_RRNEE_MERGED=0 selects the per-call-site form for comparison.
+// SP_RRNEE_MERGED=1: the lock-step IterativeRRNEE megakernel with the selection-weight estimates
+// merged across call sites (sp_path.hpp integrate_rrnee_merged; identical images).  It won while
+// both forms spilled (440 vs 395 Mrays/s on elf 1024^2 x 16 spp); built without SLP
+// vectorisation the per-call-site form needs no scratch and is faster (479 vs 452).
 static bool rrnee_merged_env()
 {
     const char* v = std::getenv("SP_RRNEE_MERGED");
-    return v ? std::atoi(v) != 0 : true;
+    return v ? std::atoi(v) != 0 : false;
 }
 
-// variant = requested waves per SIMD for __launch_bounds__ (1..4, DirectLighting only); 0 = default
+// variant = requested waves per SIMD for __launch_bounds__ (DirectLighting 1..4, IterativeRRNEE 2..4)
 KernelFn select_kernel(int integ, int variant)
 {
     switch (integ) {
@@ -32,7 +33,7 @@ KernelFn select_kernel(int integ, int variant)
     case SP_INTEGRATOR_WHITTED: return mega_recursive(integ);
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE:
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: return mega_iterative(integ, regen_env());
-    case SP_INTEGRATOR_ITERATIVE_RRNEE: return mega_rrnee(regen_env(), rrnee_merged_env());
+    case SP_INTEGRATOR_ITERATIVE_RRNEE: return mega_rrnee(regen_env(), rrnee_merged_env(), variant);
     case SP_INTEGRATOR_MANDELBROT: return mega_mandelbrot();
     default: return mega_direct(variant);
     }

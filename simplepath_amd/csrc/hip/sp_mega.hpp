@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_regen(Sc
 using KernelFn = void (*)(Scene, RenderArgs);
 KernelFn mega_direct(int variant);
 KernelFn mega_iterative(int integ, bool regen);
-KernelFn mega_rrnee(bool regen, bool merged);
+KernelFn mega_rrnee(bool regen, bool merged, int waves);
 KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 

@@ -4,11 +4,14 @@
 namespace spd {
 KernelFn mega_direct(int variant)
 {
+    // default 4 waves per SIMD (128 VGPRs) once the device code was built without SLP
+    // vectorisation: bunny 1080p @ 256 spp 2533 / 2706 Mrays/s at 3 / 4 waves, 2-way shard 1823 /
+    // 2116 / 2138 at 2 / 3 / 4 (profiles/r02/s5)
     switch (variant) {
     case 1: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, 1>;
+    case 2: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, 2>;
     case 3: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, 3>;
-    case 4: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, 4>;
-    default: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, 2>;
+    default: return sp_render_kernel<SP_INTEGRATOR_DIRECT_LIGHTING, 4>;
     }
 }
 KernelFn mega_mandelbrot() { return sp_render_kernel<SP_INTEGRATOR_MANDELBROT, 2>; }

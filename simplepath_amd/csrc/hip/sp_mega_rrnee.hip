@@ -3,11 +3,17 @@
 #include "sp_mega.hpp"
 
 namespace spd {
-KernelFn mega_rrnee(bool regen, bool merged)
+KernelFn mega_rrnee(bool regen, bool merged, int w)
 {
-    // merged: 2 waves/SIMD with 276 B/lane of scratch measured 440 Mrays/s on elf 1024^2 x 16 spp;
-    // 1 wave/SIMD (spills to AGPRs, no scratch) 285
-    if (merged && !regen) return sp_render_kernel<INTEG_RRNEE_MERGED, 2>;
-    return regen ? sp_render_regen<SP_INTEGRATOR_ITERATIVE_RRNEE, 2> : sp_render_kernel<SP_INTEGRATOR_ITERATIVE_RRNEE, 2>;
+    // Built without SLP vectorisation the per-call-site kernel fits 243 VGPRs with no scratch and
+    // is the faster form (elf 1024^2 x 16 spp: 479 vs 452 Mrays/s merged, profiles/r02/s5); the
+    // merged form (SP_RRNEE_MERGED=1) won while both spilled (440 vs 395).
+    // w = waves per SIMD (sp_render_tiles: 3 unless SP_KERNEL_VARIANT or the LDS says otherwise);
+    // elf 1024^2 x 16 spp: 476 / 553 / 519 Mrays/s at 2 / 3 / 4 waves (profiles/r02/s5)
+    if (regen) return sp_render_regen<SP_INTEGRATOR_ITERATIVE_RRNEE, 2>;
+    if (merged) return w == 2 ? sp_render_kernel<INTEG_RRNEE_MERGED, 2> : sp_render_kernel<INTEG_RRNEE_MERGED, 3>;
+    if (w == 2) return sp_render_kernel<SP_INTEGRATOR_ITERATIVE_RRNEE, 2>;
+    if (w == 4) return sp_render_kernel<SP_INTEGRATOR_ITERATIVE_RRNEE, 4>;
+    return sp_render_kernel<SP_INTEGRATOR_ITERATIVE_RRNEE, 3>;
 }
 } // namespace spd

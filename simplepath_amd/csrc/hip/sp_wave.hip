@@ -48,7 +48,8 @@ constexpr int WF_BLOCK = 256;
 #define WF_PRIM_WAVES 1 // camera-ray kernel: no occupancy request (the binary walk needs few registers)
 #endif
 #ifndef WF_TRAV_WAVES
-#define WF_TRAV_WAVES 6 // waves per SIMD requested for the traversal kernels (profiles/r01 sweep)
+#define WF_TRAV_WAVES 8 // waves per SIMD requested for wf_shadow (64 VGPRs, 20 B spill; 6 / 7 / 8 measured
+                        // 2245 / 2247 / 2282 Mrays/s without SLP vectorisation, profiles/r02/s5)
 #endif
 constexpr int QSEG     = 32; // shadow-queue segments (one counter each, QSTRIDE words apart)
 constexpr int QSTRIDE  = 32;
@@ -430,7 +431,7 @@ static size_t wave_shadow_lds(const Scene& sc) { return (size_t)(WF_BLOCK / 64) 
 static int shade_waves_env()
 {
     const char* v = std::getenv("SP_SHADE_WAVES");
-    return v ? std::atoi(v) : 4;
+    return v ? std::atoi(v) : 5; // 4 / 5 / 6 waves: 2280 / 2306 / 2236 Mrays/s (profiles/r02/s5)
 }
 static int32_t interleave_block_env()
 {
@@ -509,10 +510,10 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
     }
     const uint32_t diag_sample = diag_sample_env();
     // waves per SIMD requested for the shading kernel (register budget vs spills)
-    void (*shade)(Scene, WaveArgs, uint32_t) = wf_shade<4>;
+    void (*shade)(Scene, WaveArgs, uint32_t) = wf_shade<5>;
     switch (shade_waves_env()) {
     case 3: shade = wf_shade<3>; break;
-    case 5: shade = wf_shade<5>; break;
+    case 4: shade = wf_shade<4>; break;
     case 6: shade = wf_shade<6>; break;
     default: break;
     }

@@ -2,7 +2,7 @@
 collective runs over gloo on host copies; on a node each rank owns a GPU and bench.py gathers
 over RCCL with the same shard.gather_frame), each renders its interleaved shard with the HIP
 path, and the frame assembled on rank 0 must equal one process rendering every tile, bit for
-bit.  Shards this small run on the sample-chunk pipeline (AUTO below 12000 tiles), the full
+bit.  Shards this small run on the sample-chunk pipeline (AUTO below 24000 tiles), the full
 frame here on the wavefront, so this also checks that the two agree through the multi-rank path."""
 import os
 import socket
