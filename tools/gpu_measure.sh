@@ -12,7 +12,7 @@ bash tools/gpu_pmc_traffic.sh || exit 1
 mkdir -p gpurun_out/stats
 (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/stats/bench -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/stats/bench.json 2> $R/gpurun_out/stats/bench.err) || { echo "stats run failed"; exit 1; }
 echo "stats done"
-for pl in megakernel wavefront; do
+for pl in megakernel; do
   TAG=elf_$pl W=1024 H=1024 SPP=16 BENCH_ARGS="--scene elf --width 1024 --height 1024 --pipeline $pl" bash tools/gpu_pmc_valu.sh || exit 1
   timeout -k 10 300 python3 bench.py --no-cpu --scene elf --width 1024 --height 1024 --spp 16 --pipeline $pl > gpurun_out/elf_$pl.json 2> gpurun_out/elf_$pl.err || exit 1
   echo "elf $pl: $(python3 -c "import json;d=json.load(open('gpurun_out/elf_$pl.json'));print(d['value'],d['ms_per_step'])")"
