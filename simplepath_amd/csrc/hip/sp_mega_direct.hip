@@ -1,4 +1,8 @@
 // sp_mega_direct.hip -- DirectLighting megakernel instantiations (__launch_bounds__ variants).
+// No RNG draw-ahead window here, but the glossy estimate's words are touched in advance
+// (sp_path.hpp SP_RHO_TOUCH): 2762 vs 2720 Mrays/s with the window of 2 (profiles/r02/s5).
+#define SP_RNG_PF 0
+#define SP_RHO_TOUCH 1
 #include "sp_mega.hpp"
 
 namespace spd {

@@ -197,6 +197,17 @@ __device__ __forceinline__ void rng_reserve(Rng& r, int n)
     }
 }
 
+// SP_RHO_TOUCH: the 16-sample glossy estimate touches its 32 words first; the DMA target is one
+// 256-byte LDS sink per block.  Per translation unit: on in the DirectLighting megakernel (with
+// no draw-ahead window: bunny 2720 -> 2762 Mrays/s), off elsewhere (elf's IterativeRRNEE
+// megakernel 553 -> 541, the 8-way chunk shard unchanged; profiles/r02/s5).
+#ifndef SP_RHO_TOUCH
+#define SP_RHO_TOUCH 0
+#endif
+#if SP_RHO_TOUCH
+static __shared__ uint32_t rho_rng_sink[64];
+#endif
+
 // IncoherentSampler::get_next_1D / get_next_2D (math/Sampler.h:110-118)
 template <bool NT = false>
 __device__ __forceinline__ float next1D(Rng& r) { return canonical_from_u64(rng_raw<NT>(r)); }
@@ -1415,6 +1426,9 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
     const BeckPre p = beck_pre(m, wo, q);
     rgb           r = mkc(0, 0, 0);
     rng_reserve(rng, 32); // the loop below draws at most 32 words and never twists
+#if SP_RHO_TOUCH
+    rng_touch(rng, 32, (__attribute__((address_space(3))) void*)rho_rng_sink);
+#endif
     for (unsigned i = 0; i < 16u; ++i) {
         const MSample s = mf_sample_pre<true>(m, p, wo, rng, q);
         if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
