@@ -179,6 +179,7 @@ __device__ __forceinline__ void rng_touch(const Rng& r, int n, __attribute__((ad
 {
     const uint64_t* cur  = r.base + (size_t)r.cur * MT_N * 64;
     const uint64_t* next = r.base + (size_t)mt_next(r) * MT_N * 64;
+#pragma unroll 4
     for (int k = 0; k < n; ++k) {
         const int row = r.idx + k;
         if (row < MT_N) __builtin_amdgcn_global_load_lds((const void*)(cur + (size_t)row * 64), sink, 4, 0, 0);
