@@ -37,6 +37,10 @@ PIXEL_BYTES = 12.0  # one float3 radiance store per pixel
 SCENES = {
     "bunny": dict(writer="write_bunny_scene", file="bunny.sp", w=1920, h=1080, spp=256, integrator="direct_lighting",
                   data="synthetic (bunny-like PLY generated in-process; scene parameters of scenes/bunny.sp)"),
+    "bunny_scan": dict(writer="write_bunny_scan_scene", file="bunny_scan.sp", w=1920, h=1080, spp=256,
+                       integrator="direct_lighting",
+                       data="synthetic scan-like bunny (cupped ears, surface relief; scenes.bunny_scan_mesh), robustness "
+                            "variant of configs[2]; scene parameters of scenes/bunny.sp"),
     "spheres": dict(writer="write_material_spheres_scene", file="material_spheres_ibl.sp", w=1024, h=1024, spp=64,
                     integrator="direct_lighting",
                     data="synthetic 4096x2048 HDR night map in place of clarens_night_02_4k.pfm; scene parameters of "

@@ -79,6 +79,88 @@ def bunny_mesh(n: int = 76):
     return p.astype(np.float32), f
 
 
+def _cube_sphere(n: int):
+    """Unit-sphere vertices and outward triangles on an equal-angle cube-sphere grid (12 n^2 triangles)."""
+    t = np.tan(np.linspace(-np.pi / 4, np.pi / 4, n + 1))
+    uu, vv = np.meshgrid(t, t, indexing="ij")
+    pts, quads, base = [], [], 0
+    for axis in range(3):
+        for sign in (1.0, -1.0):
+            q = np.empty((n + 1, n + 1, 3))
+            q[..., axis] = sign
+            q[..., (axis + 1) % 3] = uu
+            q[..., (axis + 2) % 3] = vv
+            pts.append(q.reshape(-1, 3))
+            i, j = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+            v00 = base + i * (n + 1) + j
+            v10, v01, v11 = v00 + (n + 1), v00 + 1, v00 + n + 2
+            order = [v00, v10, v11, v01] if sign > 0 else [v00, v01, v11, v10]
+            quads.append(np.stack(order, -1).reshape(-1, 4))
+            base += (n + 1) * (n + 1)
+    d = np.concatenate(pts)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    _, first, inverse = np.unique(np.round(d * 1e6).astype(np.int64), axis=0, return_index=True, return_inverse=True)
+    qd = inverse.reshape(-1)[np.concatenate(quads)]
+    return d[first], np.concatenate([qd[:, [0, 1, 2]], qd[:, [0, 2, 3]]]).astype(np.int32)
+
+
+def bunny_scan_mesh(n_body: int = 70, n_ear: int = 22):
+    """A harder, scan-like bunny (robustness workload, not the headline): the body without its ear
+    lobes and with stronger surface relief, plus two separate cupped ears (closed shells whose
+    front is pressed in: concave, tilted back over the head and body), so the mesh has the
+    overhangs, creases and self-shadowing that the star-shaped stand-in lacks.  58800 + 2 x 5808
+    = 70416 triangles in the bun_zipper.ply bounding box."""
+    d, f = _cube_sphere(n_body)
+    r = np.full(d.shape[0], 1.0)
+    for c, w, a in [((0.55, 0.35, 0.0), 0.35, 0.55), ((-0.95, 0.1, 0.0), 0.08, 0.25), ((0.2, -0.9, 0.0), 0.4, -0.15)]:
+        c = np.asarray(c) / np.linalg.norm(c)
+        r += a * np.exp(-np.sum((d - c) ** 2, axis=1) / w)
+    r += 0.04 * np.sin(31.0 * d[:, 0] + 1.0) * np.cos(27.0 * d[:, 1]) * np.sin(23.0 * d[:, 2] + 0.5)
+    r += 0.02 * np.sin(57.0 * d[:, 0] * d[:, 1] + 61.0 * d[:, 2])
+    scale = np.array([1.25, 1.0, 0.8])
+    parts_v, parts_f, nv = [d * r[:, None] * scale], [f], d.shape[0]
+    e, ef = _cube_sphere(n_ear)
+    for side in (1.0, -1.0):
+        base_dir = np.array([0.35, 0.85, 0.2 * side])
+        base_dir /= np.linalg.norm(base_dir)
+        rb = 1.0 + 0.55 * np.exp(-np.sum((base_dir - np.array([0.844, 0.537, 0.0])) ** 2) / 0.35)
+        base = base_dir * rb * scale * 0.92
+        # cupped shell: the +z half is pressed through the centre plane (a concave dish)
+        q = e.copy()
+        q[:, 2] = np.where(q[:, 2] > 0.0, -0.35 * q[:, 2], q[:, 2])
+        q = q * np.array([0.16, 0.55, 0.12])
+        axis = np.array([-0.45, 1.0, 0.25 * side])
+        axis /= np.linalg.norm(axis)
+        side_v = np.cross(axis, np.array([0.0, 0.0, 1.0]))
+        side_v /= np.linalg.norm(side_v)
+        front = np.cross(side_v, axis)
+        rot = np.stack([side_v, axis, front], axis=1)  # ear x -> side, y -> axis, z (cup) -> front
+        parts_v.append(q @ rot.T + base + axis * 0.5)
+        parts_f.append(ef + nv)
+        nv += e.shape[0]
+    p = np.concatenate(parts_v)
+    lo, hi = p.min(axis=0), p.max(axis=0)
+    p = _BUNNY_LO + (p - lo) / (hi - lo) * (_BUNNY_HI - _BUNNY_LO)
+    return p.astype(np.float32), np.concatenate(parts_f).astype(np.int32)
+
+
+def write_bunny_scan_scene(directory: str) -> str:
+    """scenes/bunny.sp with bunny_scan_mesh() in place of the star-shaped stand-in."""
+    os.makedirs(directory, exist_ok=True)
+    rel = os.path.join("ply_files", "bunny", "reconstruction", "bun_scan.ply")
+    path = os.path.join(directory, rel)
+    if not os.path.exists(path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        v, f = bunny_scan_mesh()
+        tmp = path + ".tmp%d" % os.getpid()
+        write_ply(tmp, v, f)
+        os.replace(tmp, path)
+    out = os.path.join(directory, "bunny_scan.sp")
+    with open(out, "w") as fh:
+        fh.write(bunny_sp(rel))
+    return out
+
+
 def write_ply(path: str, verts: np.ndarray, faces: np.ndarray) -> None:
     """binary_little_endian PLY in the layout of bun_zipper.ply."""
     nv, nf = verts.shape[0], faces.shape[0]

@@ -17,6 +17,8 @@ def scene_dir(tmp_path_factory):
     from simplepath_amd import scenes
     d = str(tmp_path_factory.mktemp("scenes"))
     scenes.write_bunny_scene(d)
+    # the scan-like bunny (cupped ears, surface relief): a harder robustness workload
+    scenes.write_bunny_scan_scene(d)
     scenes.write_spheres_scene(d)
     # image-lit material_spheres.sp with a small synthetic HDR map (the 4k map is the bench's)
     scenes.write_material_spheres_scene(d, 96, 48, image="night_96x48.pfm")

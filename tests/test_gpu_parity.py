@@ -41,6 +41,16 @@ def test_bunny_direct_lighting_bitexact(scene_dir, pipeline):
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
 
 
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront", "chunks"])
+def test_bunny_scan_bitexact(scene_dir, pipeline):
+    # the scan-like bunny (cupped ears, surface relief; scenes.bunny_scan_mesh), reference BVH order
+    s = load(scene_dir, "bunny_scan.sp", 64, 40, bvh=1)
+    g, gst = sp.render_tiles(s, "direct_lighting", 3, pipeline=pipeline)
+    c, cst = _oracle.render(s, 6, 3, variant="spm")
+    assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
+
+
 @pytest.mark.parametrize("integrator", ["direct_lighting", "brute_force", "brute_force_iterative",
                                         "brute_force_iterative_rr", "iterative_rrnee", "whitted", "mandelbrot"])
 def test_every_integrator_bitexact(scene_dir, integrator):

@@ -111,7 +111,8 @@ def test_image_environment_light(ref, scene_dir, integrator):
     assert r.max() > 0.0
 
 
-@pytest.mark.parametrize("scene,integrator,spp", [("lucy_small.sp", "direct_lighting", 3),
+@pytest.mark.parametrize("scene,integrator,spp", [("bunny_scan.sp", "direct_lighting", 3),
+                                                  ("lucy_small.sp", "direct_lighting", 3),
                                                   ("elf_small.sp", "direct_lighting", 3),
                                                   ("elf_small.sp", "iterative_rrnee", 2)])
 def test_figure_scenes(ref, scene_dir, scene, integrator, spp):
