@@ -38,26 +38,22 @@ SP_HD double gd(const uint64_t* t, int i) { return u2d(t[i]); }
 static __shared__ uint64_t lds_exp2f_t[32];
 static __shared__ uint64_t lds_logf_t[32];
 static __shared__ uint64_t lds_powf_t[32];
-static __shared__ uint64_t lds_sincosf_t[28];
 __device__ __forceinline__ void libm_lds_init(int tid, int nthreads)
 {
     for (int i = tid; i < 32; i += nthreads) {
         lds_exp2f_t[i] = glibc::EXP2F_T[i];
         lds_logf_t[i]  = glibc::LOGF_T[i];
         lds_powf_t[i]  = glibc::POWF_T[i];
-        if (i < 28) lds_sincosf_t[i] = glibc::SINCOSF_T[i];
     }
 }
 #define SPM_EXP2F_T lds_exp2f_t
 #define SPM_LOGF_T lds_logf_t
 #define SPM_POWF_T lds_powf_t
-#define SPM_SINCOSF_T lds_sincosf_t
 #else
 SP_HD void libm_lds_init(int, int) {} // host pass / host build: tables are read in place
 #define SPM_EXP2F_T glibc::EXP2F_T
 #define SPM_LOGF_T glibc::LOGF_T
 #define SPM_POWF_T glibc::POWF_T
-#define SPM_SINCOSF_T glibc::SINCOSF_T
 #endif
 SP_HD float gf(const uint32_t* t, int i) { return u2f(t[i]); }
 
@@ -222,25 +218,32 @@ SP_HD float lm_powf(float x, float y)
 }
 
 // ------------------------------------------------------------------------------------ sinf / cosf
-// __sincosf_table[2] layout (14 doubles each): sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4
-SP_HD double sc(int tab, int k) { return gd(SPM_SINCOSF_T, tab * 14 + k); }
+// __sincosf_table[2] layout (14 doubles each): sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4.
+// Table 1 is table 0 with the cosine coefficients c0..c4 negated (sign, hpi and s1..s3 equal), so
+// no table is read at run time: table-0 constants fold into the code, a table-1 cosine polynomial
+// is the exact negation of the table-0 one (every intermediate flips sign), and sign[n & 3] is
+// {1, -1, -1, 1}.  Indexing a table by the lane's quadrant made the compiler hoist the constant-
+// index entries into 20 VGPRs for the whole kernel.
+SP_HD double sc(int k) { return gd(glibc::SINCOSF_T, k); }
 enum { SC_HPI_INV = 4, SC_HPI = 5, SC_C0 = 6, SC_C1 = 7, SC_S1 = 8, SC_C2 = 9, SC_S2 = 10, SC_C3 = 11, SC_S3 = 12, SC_C4 = 13 };
+SP_HD double sincos_sign(int q) { return (q == 1 || q == 2) ? -1.0 : 1.0; } // sign[q], q = n & 3
 
 SP_HD float sincosf_poly(double x, double x2, int tab, int n)
 {
     if ((n & 1) == 0) {
-        const double s1 = dfma(x2, sc(tab, SC_S3), sc(tab, SC_S2));
+        const double s1 = dfma(x2, sc(SC_S3), sc(SC_S2));
         const double x3 = x2 * x;
         const double x7 = x2 * x3;
-        const double s  = dfma(x3, sc(tab, SC_S1), x);
+        const double s  = dfma(x3, sc(SC_S1), x);
         return (float)dfma(s1, x7, s);
     }
     const double x4 = x2 * x2;
-    const double c1 = dfma(x2, sc(tab, SC_C1), sc(tab, SC_C0));
-    const double c2 = dfma(x2, sc(tab, SC_C4), sc(tab, SC_C3));
+    const double c1 = dfma(x2, sc(SC_C1), sc(SC_C0));
+    const double c2 = dfma(x2, sc(SC_C4), sc(SC_C3));
     const double x6 = x2 * x4;
-    const double c  = dfma(x4, sc(tab, SC_C2), c1);
-    return (float)dfma(c2, x6, c);
+    const double c  = dfma(x4, sc(SC_C2), c1);
+    const float  r  = (float)dfma(c2, x6, c);
+    return tab ? -r : r;
 }
 
 SP_HD double sincosf_reduce_large(uint32_t xi, int* np)
@@ -276,10 +279,10 @@ SP_HD float lm_sinf(float y)
         return sincosf_poly(x, s, 0, 0);
     }
     if (BOUNDED || abstop <= 0x42eu) {
-        const double r  = x * sc(0, SC_HPI_INV);
+        const double r  = x * sc(SC_HPI_INV);
         int          n  = (((int32_t)r) + 0x800000) >> 24;
-        x               = dfma(-(double)n, sc(0, SC_HPI), x);
-        const double sg = sc(0, n & 3);
+        x               = dfma(-(double)n, sc(SC_HPI), x);
+        const double sg = sincos_sign(n & 3);
         const int    tb = (n & 2) ? 1 : 0;
         return sincosf_poly(x * sg, x * x, tb, n);
     }
@@ -287,7 +290,7 @@ SP_HD float lm_sinf(float y)
         const int sign = (int)(iy >> 31);
         int       n;
         x               = sincosf_reduce_large(iy, &n);
-        const double sg = sc(0, (n + sign) & 3);
+        const double sg = sincos_sign((n + sign) & 3);
         const int    tb = ((n + sign) & 2) ? 1 : 0;
         return sincosf_poly(x * sg, x * x, tb, n);
     }
@@ -307,10 +310,10 @@ SP_HD float lm_cosf(float y)
         return sincosf_poly(x, s, 0, 1);
     }
     if (BOUNDED || abstop <= 0x42eu) {
-        const double r  = x * sc(0, SC_HPI_INV);
+        const double r  = x * sc(SC_HPI_INV);
         int          n  = (((int32_t)r) + 0x800000) >> 24;
-        x               = dfma(-(double)n, sc(0, SC_HPI), x);
-        const double sg = sc(0, n & 3);
+        x               = dfma(-(double)n, sc(SC_HPI), x);
+        const double sg = sincos_sign(n & 3);
         const int    tb = (n & 2) ? 1 : 0;
         return sincosf_poly(x * sg, x * x, tb, n ^ 1);
     }
@@ -318,7 +321,7 @@ SP_HD float lm_cosf(float y)
         const int sign = (int)(iy >> 31);
         int       n;
         x               = sincosf_reduce_large(iy, &n);
-        const double sg = sc(0, (n + sign) & 3);
+        const double sg = sincos_sign((n + sign) & 3);
         const int    tb = ((n + sign) & 2) ? 1 : 0;
         return sincosf_poly(x * sg, x * x, tb, n ^ 1);
     }
