@@ -60,7 +60,57 @@ struct Rng {
 __device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_N * 64; }
 __device__ __forceinline__ int       mt_next(const Rng& r) { return r.lin ? r.cur + 1 : r.cur ^ 1; }
 
-// B = twist(A) without modifying A (in-place MT19937-64 twist split over two buffers).
+// B = twist(A) without modifying A (in-place MT19937-64 twist split over two buffers), for twists
+// at points where few registers are live (rng_prepare at a sample start, rng_skip).  A and B are
+// different generations (__restrict__), and the words are processed in blocks of U words:
+// a block's loads are all issued before its first store.  Without that the compiler had to assume
+// that a store to B could change A, so every 4-word step waited for its loads to return before
+// the next step's loads were issued -- about 80 dependent memory round trips per twist.
+// Block sizes, measured (profiles/r02/s6/ab_twist.txt): 12 at rng_prepare (bunny 1080p 2815-2858 ->
+// 2949-2955 Mrays/s, elf 554 -> 586; 16 and 24 spill around the sample loop: elf 411 at 24), 24 in
+// the chunk pipeline's stream replay (ck_count, few other live values: 8-way shard 2150 -> 2360).
+#ifndef SP_TWIST_BLOCK
+#define SP_TWIST_BLOCK 12
+#endif
+#ifndef SP_TWIST_SKIP_BLOCK
+#define SP_TWIST_SKIP_BLOCK 24
+#endif
+// words k .. k + NW - 1 of B; the words mixed in come from A[k + M] (first part) or B[k - (N - M)]
+template <int NW, bool SECOND>
+__device__ __forceinline__ void mt_twist_words(const uint64_t* __restrict__ A, uint64_t* __restrict__ B, int k, uint64_t& ak)
+{
+    if constexpr (NW > 0) {
+        uint64_t a1[NW], am[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            a1[j] = A[(k + j + 1) * 64];
+            am[j] = SECOND ? B[(k + j - (MT_N - MT_M)) * 64] : A[(k + j + MT_M) * 64];
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            B[(k + j) * 64] = am[j] ^ mt_mix(ak, a1[j]);
+            ak              = a1[j];
+        }
+    }
+}
+template <int U>
+__device__ __forceinline__ void mt_twist_blocked(const uint64_t* __restrict__ A, uint64_t* __restrict__ B)
+{
+    constexpr int H  = MT_N - MT_M;     // words 0 .. H - 1 mix with A[k + M]
+    constexpr int N2 = MT_N - 1 - H;    // words H .. N - 2 mix with B[k - H]
+    uint64_t      ak = A[0];
+#pragma unroll 1
+    for (int b = 0; b < H / U; ++b) mt_twist_words<U, false>(A, B, b * U, ak);
+    mt_twist_words<H % U, false>(A, B, (H / U) * U, ak);
+#pragma unroll 1
+    for (int b = 0; b < N2 / U; ++b) mt_twist_words<U, true>(A, B, H + b * U, ak);
+    mt_twist_words<N2 % U, true>(A, B, H + (N2 / U) * U, ak);
+    B[(MT_N - 1) * 64] = B[(MT_M - 1) * 64] ^ mt_mix(ak, B[0]);
+}
+
+// B = twist(A) without modifying A: the compact form, for twists inside register-heavy code (the
+// in-draw fallback, rng_reserve), where the blocked form's 4 x SP_TWIST_BLOCK live registers would
+// spill.
 __device__ __forceinline__ void mt_twist_into(const uint64_t* A, uint64_t* B)
 {
     uint64_t ak = A[0];
@@ -109,7 +159,7 @@ __device__ __forceinline__ void rng_prepare(Rng& r)
     const bool urgent = !r.ready && r.idx >= MT_N - RNG_MARGIN;
     if (__any(urgent)) {
         if (!r.ready) {
-            mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+            mt_twist_blocked<SP_TWIST_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
             r.ready = 1;
         }
     }
@@ -155,7 +205,7 @@ __device__ __forceinline__ void rng_skip(Rng& r, int n)
 {
     while (n > 0) {
         if (r.idx >= MT_N) {
-            if (!r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+            if (!r.ready) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
             r.cur   = mt_next(r);
             r.idx   = 0;
             r.ready = r.pre;
