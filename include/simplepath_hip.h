@@ -189,7 +189,8 @@ typedef struct sp_render_params {
 
 /* Device pipeline selection (sp_render_params.flags).  All produce identical images. */
 enum {
-    SP_PIPELINE_AUTO       = 0, /* by work size: wavefront / megakernel / sample chunks (below)   */
+    SP_PIPELINE_AUTO       = 0, /* by work size: megakernel, or sample chunks for DirectLighting
+                                   below 24000 tiles when their buffers fit     */
     SP_PIPELINE_MEGAKERNEL = 1, /* one lane owns one pixel for all samples (sp_mega.hpp)        */
     SP_PIPELINE_WAVEFRONT  = 2, /* DirectLighting: per-sample primary/shade/shadow kernels       */
     SP_PIPELINE_SAMPLE_CHUNKS = 3, /* DirectLighting: each pixel's samples in parallel chunks
