@@ -23,12 +23,16 @@
 // (tests/test_gpu_parity.py).  Camera rays are traced once, and each generation of a stream is
 // twisted once.  HBM per pixel-sample: 16 B hit record + 2 B draw count + 12 B radiance written
 // and read back; per pixel: 2.5 KB per 312 draws of generator store.
-// RNG draw-ahead window (sp_path.hpp Rng): ck_shade reads a generator store that ck_count wrote
-// long before, so every draw is an HBM read; look further ahead than the megakernel does.
+// ck_shade reads a generator store that ck_count wrote long before, so every draw is an HBM read.
+// As in the DirectLighting megakernel, the glossy estimate's 32 words are touched in advance
+// (SP_RHO_TOUCH, LDS-DMA into a sink) and no draw-ahead window holds registers: 8-way shard
+// 2359-2368 -> 2428-2456 Mrays/s, 2-way 2555 -> 2659, against a window of 2 without the touch
+// (profiles/r02/s6/ab_chunk_touch.txt).
 #ifndef SP_CHUNK_RNG_PF
-#define SP_CHUNK_RNG_PF 2
+#define SP_CHUNK_RNG_PF 0
 #endif
 #define SP_RNG_PF SP_CHUNK_RNG_PF
+#define SP_RHO_TOUCH 1
 #include "sp_chunk.hpp"
 
 #include <cstdlib>
