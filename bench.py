@@ -72,16 +72,23 @@ def parse():
                          "else os.cpu_count())")
     ap.add_argument("--parity-seconds", type=float, default=6.0,
                     help="N > 1: CPU budget for the parity sample of the gathered frame")
+    ap.add_argument("--pg-timeout", type=float, default=1800.0,
+                    help="N > 1: collective timeout (s) of the process group; only the render and the gather "
+                         "run inside it -- rank 0's reference scene build and parity run after teardown")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="test hook: spawn the ranks like --gpus N does, join a gloo group, no GPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront", "chunks"])
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_bench_bunny.json"))
-    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "pmc_valu_bench_bunny.json"),
-                    help="tools/pmc_valu.py output of a PMC pass of this workload (VALU-issue roofline)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="tools/pmc_traffic.py output of this workload (default profiles/pmc_bench_<scene>.json)")
+    ap.add_argument("--valu-json", default=None,
+                    help="tools/pmc_valu.py output of a PMC pass of this workload (VALU-issue roofline; default "
+                         "profiles/pmc_valu_bench_<scene>.json)")
     a = ap.parse_args()
+    a.traffic_json = a.traffic_json or os.path.join(ROOT, "profiles", f"pmc_bench_{a.scene}.json")
+    a.valu_json = a.valu_json or os.path.join(ROOT, "profiles", f"pmc_valu_bench_{a.scene}.json")
     sc = SCENES[a.scene]
     a.width = a.width or sc["w"]
     a.height = a.height or sc["h"]
@@ -112,12 +119,29 @@ def self_launch(args) -> int:
     return subprocess.run(cmd).returncode
 
 
+def affinity_cpus() -> int:
+    """CPUs the scheduler lets this process run on (os.sched_getaffinity)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_share() -> int:
     """CPUs this process may use: the GPU box gives each GPU a share (OMP_NUM_THREADS), while
-    os.cpu_count() reports the whole machine there."""
-    n = os.cpu_count() or 1
+    os.cpu_count() reports the whole machine there; never more than the affinity mask allows."""
+    n = min(os.cpu_count() or 1, affinity_cpus())
     omp = os.environ.get("OMP_NUM_THREADS", "")
     return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else n
+
+
+class _CpuStats:
+    """RenderStats stand-in of the SP_BENCH_CPU_RENDER test hook (oracle render on the host)."""
+
+    def __init__(self, st, ms):
+        self.rays, self.shadow_rays, self.samples = int(st["rays"]), int(st["shadow_rays"]), int(st["samples"])
+        self.rng_draws, self.kernel_ms, self.pipeline, self.primary_hits = 0, ms, 1, 0
+        self.stage_ms, self.parts, self.stack_depth, self.launches = (ms, 0.0, 0.0, 0.0), 1, 0, 1
 
 
 def main():
@@ -138,27 +162,41 @@ def main():
                   flush=True)
         dist.destroy_process_group()
         return
+    import datetime
+
     import torch
 
     dist = None
     # SP_BENCH_SHARED_DEVICE=1 (test hook): every rank renders on cuda:0 and the ranks talk over
-    # gloo with host copies -- the N>1 flow on a one-GPU box (RCCL needs one GPU per rank)
-    shared = world > 1 and os.environ.get("SP_BENCH_SHARED_DEVICE") == "1"
+    # gloo with host copies -- the N>1 flow on a one-GPU box (RCCL needs one GPU per rank).
+    # SP_BENCH_CPU_RENDER=1 (test hook, no GPU): the CPU oracle renders each rank's shard and the
+    # ranks talk over gloo -- the orchestration (timeouts, teardown before rank 0's reference work)
+    # exercised on CPU (tests/test_multi_rank.py).
+    cpu_render = os.environ.get("SP_BENCH_CPU_RENDER") == "1"
+    shared = world > 1 and (os.environ.get("SP_BENCH_SHARED_DEVICE") == "1" or cpu_render)
+    pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
     if world > 1:
         import torch.distributed as dist
 
         if shared:
             local = 0
-            torch.cuda.set_device(0)
-            dist.init_process_group("gloo")
+            if not cpu_render:
+                torch.cuda.set_device(0)
+            dist.init_process_group("gloo", timeout=pg_timeout)
         else:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), timeout=pg_timeout)
         world = dist.get_world_size()
     else:
-        torch.cuda.set_device(0)
+        if not cpu_render:
+            torch.cuda.set_device(0)
         local = 0
     cdev = "cpu" if shared else f"cuda:{local}"  # where the collectives' tensors live
+    rdev = "cpu" if cpu_render else f"cuda:{local}"  # where the render output lives
+
+    def sync():
+        if not cpu_render:
+            torch.cuda.synchronize()
 
     import simplepath_amd as sp
     from simplepath_amd import scenes
@@ -172,7 +210,8 @@ def main():
     path = os.path.join(scene_dir, fname)
     scene = sp.Scene.from_file(path)
     scene.set_resolution(args.width, args.height)
-    scene.upload(device=local, bvh_mode=args.bvh)
+    if not cpu_render:
+        scene.upload(device=local, bvh_mode=args.bvh)
     integ = sp.string_to_integrator_type(args.integrator)
 
     from simplepath_amd import shard
@@ -184,18 +223,32 @@ def main():
     if args.sim_world > 1 and world == 1:
         my_tiles = shard.shard_tiles(n_tiles, 0, args.sim_world)
         per_rank = shard.per_rank_capacity(n_tiles, args.sim_world)
-    out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=f"cuda:{local}")
+    out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=rdev)
     gathered, frame = None, None
     if dist is not None and rank == 0:
         gathered = [torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=cdev) for _ in range(world)]
         frame = torch.zeros((n_tiles, 64, 3), dtype=torch.float32, device=cdev)
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = None if cpu_render else torch.cuda.current_stream().cuda_stream
     gather_ms = []
 
+    def render():
+        if cpu_render:
+            from tests import _oracle
+            t = time.perf_counter()
+            tiles, st = _oracle.render(scene, integ, args.spp, my_tiles, threads=2, variant="glibc")
+            out[: len(my_tiles)] = torch.from_numpy(tiles)
+            return _CpuStats(st, (time.perf_counter() - t) * 1e3)
+        return sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
+                                      pipeline=args.pipeline, stage_timing=True)
+
     def step():
-        st = sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
-                                    pipeline=args.pipeline, stage_timing=True)
+        st = render()
         if dist is not None:  # single RCCL gather of the tile buffers at frame end
+            if cpu_render:
+                t = time.perf_counter()
+                shard.gather_frame(out, n_tiles, rank, world, dist, gathered, frame)
+                gather_ms.append((time.perf_counter() - t) * 1e3)
+                return st
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             shard.gather_frame(out if not shared else out.cpu(), n_tiles, rank, world, dist, gathered, frame)
@@ -205,25 +258,26 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     stats = []
     for _ in range(args.steps):
         stats.append(step())
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     rays = sum(s.rays for s in stats)
     samples = sum(s.samples for s in stats)
     draws = sum(s.rng_draws for s in stats)
     kernel_ms = sum(s.kernel_ms for s in stats) / max(1, len(stats))
     timed_gathers = gather_ms[-args.steps:] if gather_ms else []
-    g_ms = sum(a.elapsed_time(b) for a, b in timed_gathers) / len(timed_gathers) if timed_gathers else 0.0
+    g_ms = (sum(g if isinstance(g, float) else g[0].elapsed_time(g[1]) for g in timed_gathers) / len(timed_gathers)
+            if timed_gathers else 0.0)
     rank_info = None
     if dist is not None:
         t = torch.tensor([elapsed, float(rays), float(samples), float(draws)], dtype=torch.float64, device=cdev)
@@ -237,14 +291,21 @@ def main():
         dist.all_gather(every, mine)
         rank_info = [{"rank": r, "tiles": int(v[0]), "gather_ms": round(float(v[1]), 3),
                       "render_ms": round(float(v[2]), 2)} for r, v in enumerate(x.cpu().numpy() for x in every)]
-    if rank != 0:
-        dist.barrier()  # rank 0 checks parity of the gathered frame before the group is torn down
+        # Every rank leaves the group here.  What follows on rank 0 -- the reference scene build
+        # (minutes for lucy's 28 M triangles) and the parity check of the gathered frame -- needs
+        # no collective, so no rank waits on it inside a collective timeout.
+        dist.barrier()
         dist.destroy_process_group()
+    if rank != 0:
         return
+    stall = float(os.environ.get("SP_BENCH_POST_STALL_S", "0") or 0)  # test hook: a slow reference build
+    if stall > 0:
+        time.sleep(stall)
 
     mrays = rays / elapsed / 1e6
     msamples = samples / elapsed / 1e6
-    roofline = roofline_of(stats, min(len(my_tiles) * 64, args.width * args.height), args, kernel_ms)
+    roofline = None if cpu_render else roofline_of(stats, min(len(my_tiles) * 64, args.width * args.height), args,
+                                                   kernel_ms)
 
     cpu = None
     parity = None
@@ -281,7 +342,8 @@ def main():
         "config": {"workload": f"{fname} {args.width}x{args.height} @ {args.spp} spp, {args.integrator}",
                    "width": args.width, "height": args.height, "spp": args.spp, "integrator": args.integrator,
                    "bvh": "sah" if args.bvh == 0 else "reference", "tiles": int(n_tiles),
-                   "pipeline": ["auto", "megakernel", "wavefront", "chunks"][stats[-1].pipeline],
+                   "pipeline": "cpu-oracle (test hook)" if cpu_render else
+                               ["auto", "megakernel", "wavefront", "chunks"][stats[-1].pipeline],
                    "parallelism": f"tiles{world}"},
         "msamples_per_s": round(msamples, 3),
         "rays_per_step": rays / args.steps,
@@ -293,13 +355,20 @@ def main():
         line["world_size"] = world
         if shared:
             line["test_shared_device"] = True  # not a multi-GPU measurement
+        if cpu_render:
+            line["test_cpu_render"] = True  # oracle on the host: orchestration test, not a measurement
         line["gather_ms"] = round(g_ms, 3)
+        ms_step = elapsed / args.steps * 1e3
+        render = [r["render_ms"] for r in rank_info]
+        # per-rank render time: slowest over mean (1.0 = perfectly balanced shards); the gather's
+        # share of a step (rank 0's gather, HIP events around the RCCL call)
+        line["imbalance"] = round(max(render) / max(1e-9, sum(render) / len(render)), 4)
+        line["gather_frac"] = round(g_ms / max(1e-9, ms_step), 5)
         line["ranks"] = rank_info
+        if stall > 0:
+            line["test_post_stall_s"] = stall
     print(json.dumps(line), flush=True)
     os.dup2(2, 1)  # exit-time log summaries of the reference library go to stderr
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 def stage_bytes(st, pixels):
@@ -326,8 +395,8 @@ def valu_of(args, kernel):
             vj = json.load(fh)
     except (OSError, ValueError):
         return None
-    if (vj.get("width"), vj.get("height"), vj.get("spp"), vj.get("scene", "bunny")) != \
-            (args.width, args.height, args.spp, args.scene):
+    if (vj.get("width"), vj.get("height"), vj.get("spp"), vj.get("scene", "bunny"), vj.get("sim_world", 0)) != \
+            (args.width, args.height, args.spp, args.scene, args.sim_world):
         return None
     k = vj.get("kernels", {}).get(kernel)
     if not k:
@@ -349,7 +418,7 @@ def roofline_of(stats, pixels, args, kernel_ms):
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
             if (tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp
-                    and tj.get("scene", "bunny") == args.scene):
+                    and tj.get("scene", "bunny") == args.scene and tj.get("sim_world", 0) == args.sim_world):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -465,6 +534,7 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles, budget_s):
                      f"{t_used:.1f} s, " + ("oracle/_ref/libsp_ref.so = reference sources" if ref is not None
                                              else "oracle liboracle_glibc.so") + ")",
            "msamples_per_s": round(st["samples"] / t_used / 1e6, 5), "host_cores": os.cpu_count(),
+           "affinity_cpus": affinity_cpus(),
            "build": REF_BUILD if ref is not None else "oracle/Makefile: gcc -O2 -mavx2 -mfma -ffp-contract=off"}
     parity = {"vs": kind, "tiles": len(done)}
     if ref is not None:

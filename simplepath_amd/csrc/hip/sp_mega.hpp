@@ -38,6 +38,9 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
     const int rs_words = rsqrt_words(sc);
     for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
+#ifdef SP_WAVE_PROF
+    if (lane < 8) wprof_lds[wave * 8 + lane] = 0;
+#endif
     __syncthreads();
     Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
     Stack st{ lds + rs_words + wave * sc.stack_words * 64, lane, sc.stack_depth };
@@ -85,7 +88,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
                 if constexpr (INTEG == SP_INTEGRATOR_MANDELBROT)
                     acc = cadd(acc, integrate_mandelbrot(fx, fy, sc.width, sc.height));
                 else
-                    acc = cadd(acc, integrate<INTEG>(c, ray)); // image(p) += integrate(...)
+                    SP_WPROF(0, acc = cadd(acc, integrate<INTEG>(c, ray))); // image(p) += integrate(...)
             }
             acc = cdivs(acc, (float)args.spp); // image(p) /= num_pixel_samples
 #ifdef SP_MEGA_PROF
@@ -100,6 +103,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         o[0]     = acc.r;
         o[1]     = acc.g;
         o[2]     = acc.b;
+#ifndef SP_WAVE_PROF
         if (args.tile_diag) {
             // {t0, t1, wave, item, then per stage the largest shader-clock total of any lane}
             for (int k = 0; k < 4; ++k)
@@ -111,7 +115,11 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
             const uint64_t rec[8] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item, prof[0], prof[1], prof[2], prof[3] };
             if (lane < 8) args.tile_diag[(size_t)slot * 8 + lane] = rec[lane];
         }
+#endif
     }
+#ifdef SP_WAVE_PROF
+    if (args.tile_diag && lane < 8) atomicAdd(args.tile_diag + lane, wprof_lds[wave * 8 + lane]);
+#endif
     unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
     for (int k = 0; k < 4; ++k) {
         unsigned long long s = v[k];

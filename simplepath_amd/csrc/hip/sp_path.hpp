@@ -19,6 +19,36 @@ namespace spd {
 
 using namespace spm;
 
+// ============================================================================ wave-level profile
+// Diagnostic build only (-DSP_WAVE_PROF, tools/gpu_wprof.sh): for each region k the wave's shader
+// clocks inside it (slot 2k) and those clocks times the lanes active in it (slot 2k + 1), so the
+// region's share of wave time and its lane occupancy come out separately.  Regions:
+// 0 = a whole sample (integrate), 1 = the 16-sample glossy rho estimate, 2 = BVH / light queries,
+// 3 = the MT twist at rng_prepare.  Written by the first active lane into a per-wave LDS row,
+// flushed to the render's tile_diag buffer at kernel end (sp_mega.hpp).
+#ifdef SP_WAVE_PROF
+static __shared__ unsigned long long wprof_lds[16 * 8];
+__device__ __forceinline__ void wprof_end(int k, uint64_t t0)
+{
+    const uint64_t dt    = __builtin_amdgcn_s_memtime() - t0;
+    const uint64_t m     = __ballot(1);
+    const int      first = __ffsll((unsigned long long)m) - 1;
+    if ((int)(threadIdx.x & 63) == first) {
+        const int w = threadIdx.x >> 6;
+        wprof_lds[w * 8 + 2 * k] += dt;
+        wprof_lds[w * 8 + 2 * k + 1] += dt * (uint64_t)__popcll(m);
+    }
+}
+#define SP_WPROF(k, stmt)                                                                                              \
+    do {                                                                                                               \
+        const uint64_t t_wp_ = __builtin_amdgcn_s_memtime();                                                           \
+        stmt;                                                                                                          \
+        wprof_end(k, t_wp_);                                                                                           \
+    } while (0)
+#else
+#define SP_WPROF(k, stmt) stmt
+#endif
+
 // ============================================================================ per-lane state
 struct Rsq {
     const uint32_t* t;
@@ -159,7 +189,7 @@ __device__ __forceinline__ void rng_prepare(Rng& r)
     const bool urgent = !r.ready && r.idx >= MT_N - RNG_MARGIN;
     if (__any(urgent)) {
         if (!r.ready) {
-            mt_twist_blocked<SP_TWIST_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+            SP_WPROF(3, mt_twist_blocked<SP_TWIST_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r))));
             r.ready = 1;
         }
     }
@@ -1490,7 +1520,8 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
 // OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
 __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
 {
-    const rgb r0 = mf_rho16(m, wo, rng, q);
+    rgb r0;
+    SP_WPROF(1, r0 = mf_rho16(m, wo, rng, q));
     const rgb r1 = cscale(m.lambert_albedo, k_pi); // LambertianBRDF::rho_impl
     float     sum = 0.0f;
     w[0] = luminance(r0);
@@ -1805,7 +1836,9 @@ __device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float
 {
     ++c.shadow;
     ++c.rays;
-    return scene_any(c.sc, r, tmin, tmax, c.st);
+    bool hit;
+    SP_WPROF(2, hit = scene_any(c.sc, r, tmin, tmax, c.st));
+    return hit;
 }
 
 // Shared "primary" query of every integrator: intersect_lights then intersect.
@@ -1818,9 +1851,12 @@ __device__ __forceinline__ Query trace(Ctx& c, const Ray& ray, float tmin, float
 {
     Query qr;
     ++c.rays;
-    qr.lh = scene_intersect_lights(c.sc, ray, tmin, tmax, c.st);
-    if (qr.lh.hit) tmax = qr.lh.t;
-    const Hit h = scene_intersect(c.sc, ray, tmin, tmax, c.st);
+    Hit h;
+    SP_WPROF(2, {
+        qr.lh = scene_intersect_lights(c.sc, ray, tmin, tmax, c.st);
+        if (qr.lh.hit) tmax = qr.lh.t;
+        h = scene_intersect(c.sc, ray, tmin, tmax, c.st);
+    });
     qr.geom     = (h.code != 0xffffffffu);
     if (qr.geom) qr.is = finish_hit(c.sc, h, ray, c.q);
     return qr;
@@ -2026,7 +2062,8 @@ __device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p,
     mr.d             = ms.dir;
     const float mmin = ray_offset(n, ms.dir);
     ++c.rays;
-    const LightHit lh = scene_intersect_lights(c.sc, mr, mmin, k_infinite, c.st);
+    LightHit lh;
+    SP_WPROF(2, lh = scene_intersect_lights(c.sc, mr, mmin, k_infinite, c.st));
     if (lh.hit) {
         if (!occluded(c, mr, mmin, k_infinite))
             Lr = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, light_hit_L(c.sc, lh, mr.d, c.q)), abs_f(dot(ms.dir, n))), w), ms.pdf));

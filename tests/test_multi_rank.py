@@ -102,3 +102,28 @@ def test_bench_launch_command():
     assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
     assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
     assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
+
+
+@pytest.mark.timeout(400)
+def test_bench_rank0_reference_work_after_teardown(scene_dir):
+    """bench.py --gpus 2 (CPU oracle renders, gloo): rank 0's post-render work -- the reference
+    scene build and the parity check of the gathered frame, minutes for lucy -- runs after every
+    rank has left the process group.  A stall of 3x the collective timeout must not abort the run
+    (before round 3 the other ranks waited in a barrier inside that timeout)."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, SP_BENCH_CPU_RENDER="1", SP_BENCH_POST_STALL_S="15", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--width", "40", "--height", "24", "--spp", "2", "--pg-timeout", "5",
+                        "--parity-seconds", "1"],
+                       capture_output=True, text=True, timeout=380, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["test_cpu_render"] and line["test_post_stall_s"] == 15.0 and line["world_size"] == 2
+    assert sum(x["tiles"] for x in line["ranks"]) == line["config"]["tiles"] == 15
+    assert line["imbalance"] >= 1.0 and 0.0 <= line["gather_frac"] < 1.0
+    p = line["parity"]
+    assert p["frame"] == "gathered" and p["tiles"] > 0 and p["rel_l2"] == 0.0

@@ -1,21 +1,31 @@
 #!/bin/bash
-# GPU tests, then the BASELINE configs beyond the default line: lucy 1080p@256 (N=1 and the 8-way
-# shard), elf 4096^2@1024 max-depth 16 (the 8-way shard), spheres (N=1), the scan-like bunny (N=1),
-# bunny's 2/4/8-way shards.  SKIP_TESTS=1 skips the test suite.
+# The BASELINE configs beyond the default line, each with the reference CPU path timed beside it
+# (cpu_baseline, kind "reference") and parity of the GPU frame against it:
+#   spheres (configs[1], N=1), lucy (configs[3]: the 1-GPU frame and one rank's 8-way shard),
+#   elf (configs[4]: one rank's 8-way shard), bunny's 2/4/8-way shards, the scan-like bunny.
+# CONFIGS selects a subset (space-separated names); PMC=1 adds the VALU-roofline PMC passes of
+# each line's workload (tools/gpu_pmc_valu.sh) so its roofline.valu is filled on a rerun.
 set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
 mkdir -p gpurun_out/cfg
-if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/cfg/tests.log 2>&1 || { tail -30 gpurun_out/cfg/tests.log; exit 1; }
-  tail -2 gpurun_out/cfg/tests.log
-fi
-run() { # name, args
-  local n=$1; shift
-  timeout -k 10 300 python -u bench.py --no-cpu "$@" > gpurun_out/cfg/$n.json 2> gpurun_out/cfg/$n.err || { tail -5 gpurun_out/cfg/$n.err; exit 1; }
-  echo "$n $(python -c "import json;d=json.load(open('gpurun_out/cfg/$n.json'));print(d['value'],d['ms_per_step'],d['config']['pipeline'],d['config']['workload'])")"
-}
-run spheres --scene spheres --steps 2 --warmup 1
-run bunny_scan --scene bunny_scan --steps 2 --warmup 1
-for n in 2 4 8; do run bunny_shard$n --steps 2 --warmup 1 --sim-world $n; done
-run lucy1 --scene lucy --steps 2 --warmup 1
-run lucy8 --scene lucy --steps 2 --warmup 1 --sim-world 8
-run elf8 --scene elf --steps 1 --warmup 0 --sim-world 8
+declare -A A=(
+  [spheres]="--scene spheres --steps 2 --warmup 1"
+  [bunny_scan]="--scene bunny_scan --steps 2 --warmup 1"
+  [bunny_shard2]="--steps 2 --warmup 1 --sim-world 2"
+  [bunny_shard4]="--steps 2 --warmup 1 --sim-world 4"
+  [bunny_shard8]="--steps 2 --warmup 1 --sim-world 8"
+  [lucy1]="--scene lucy --steps 2 --warmup 1"
+  [lucy8]="--scene lucy --steps 2 --warmup 1 --sim-world 8"
+  [elf8]="--scene elf --steps 1 --warmup 0 --sim-world 8"
+)
+for n in ${CONFIGS:-spheres bunny_scan bunny_shard2 bunny_shard4 bunny_shard8 lucy1 lucy8 elf8}; do
+  timeout -k 10 1000 python -u bench.py ${A[$n]} ${BENCH_ARGS:-} > gpurun_out/cfg/$n.json 2> gpurun_out/cfg/$n.err || { tail -5 gpurun_out/cfg/$n.err; exit 1; }
+  echo "$n $(python -c "import json;d=json.load(open('gpurun_out/cfg/$n.json'));c=d['cpu_baseline'] or {};p=d['parity'] or {};print(d['value'],d['ms_per_step'],d['config']['pipeline'],'cpu',c.get('value'),'parity',p.get('rel_l2'),p.get('bitexact_pixel_frac'))")"
+  if [ -n "${PMC:-}" ]; then
+    sc=$(python -c "import sys;a=sys.argv[1:];print(a[a.index('--scene')+1] if '--scene' in a else 'bunny')" ${A[$n]})
+    sw=$(python -c "import sys;a=sys.argv[1:];print(a[a.index('--sim-world')+1] if '--sim-world' in a else 0)" ${A[$n]})
+    SCENE=$sc SIMW=$sw TAG=$n bash tools/gpu_pmc_valu.sh > gpurun_out/cfg/pmc_$n.log 2>&1 || { tail -5 gpurun_out/cfg/pmc_$n.log; exit 1; }
+    tail -2 gpurun_out/cfg/pmc_$n.log
+  fi
+done

@@ -37,6 +37,8 @@ def per_kernel(root, counter):
 
 def main():
     root, w, h, spp, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+    scene = sys.argv[6] if len(sys.argv) > 6 else "bunny"  # bench.py --scene of the profiled run
+    sim_world = int(sys.argv[7]) if len(sys.argv) > 7 else 0  # bench.py --sim-world of the profiled run
     fetch = per_kernel(os.path.join(root, "p1"), "FETCH_SIZE")
     write = per_kernel(os.path.join(root, "p2"), "WRITE_SIZE")
     kernels = {}
@@ -50,7 +52,7 @@ def main():
         kernels[k.replace("spd::", "")] = {"dispatches": n, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                                            "hbm_bytes_per_launch": fb + wb}
     dom = "wf_shade" if "wf_shade" in kernels else max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
-    res = {"width": w, "height": h, "spp": spp, "kernel": dom,
+    res = {"width": w, "height": h, "spp": spp, "scene": scene, "sim_world": sim_world, "kernel": dom,
            "hbm_bytes_per_launch": kernels[dom]["hbm_bytes_per_launch"], "kernels": kernels,
            "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1, KiB -> bytes"}
     with open(out, "w") as fh:

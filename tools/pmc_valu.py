@@ -64,6 +64,8 @@ def mean(x):
 
 def main():
     root, w, h, spp, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+    scene = sys.argv[6] if len(sys.argv) > 6 else "bunny"  # bench.py --scene of the profiled run
+    sim_world = int(sys.argv[7]) if len(sys.argv) > 7 else 0  # bench.py --sim-world of the profiled run
     vals, durs = load(root)
     res = {}
     for k, c in vals.items():
@@ -93,7 +95,7 @@ def main():
             if n in m:
                 d[n] = m[n]
         res[k] = d
-    doc = {"width": w, "height": h, "spp": spp, "model": __doc__.split("Usage:")[0].strip(), "kernels": res}
+    doc = {"width": w, "height": h, "spp": spp, "scene": scene, "sim_world": sim_world, "model": __doc__.split("Usage:")[0].strip(), "kernels": res}
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
     for k, d in sorted(res.items(), key=lambda x: -x[1]["valu_cycles"] * x[1]["dispatches"]):
