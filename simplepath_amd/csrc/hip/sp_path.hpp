@@ -23,8 +23,9 @@ using namespace spm;
 // Diagnostic build only (-DSP_WAVE_PROF, tools/gpu_wprof.sh): for each region k the wave's shader
 // clocks inside it (slot 2k) and those clocks times the lanes active in it (slot 2k + 1), so the
 // region's share of wave time and its lane occupancy come out separately.  Regions:
-// 0 = a whole sample (integrate), 1 = the 16-sample glossy rho estimate, 2 = BVH / light queries,
-// 3 = the MT twist at rng_prepare.  Written by the first active lane into a per-wave LDS row,
+// 0 = a whole sample (integrate), 1 = the 16-sample glossy rho estimate, 2 = closest-hit queries
+// (camera / extension rays: their entry occupancy is the fraction of paths alive), 3 = shadow and
+// MIS-ray queries.  Written by the first active lane into a per-wave LDS row,
 // flushed to the render's tile_diag buffer at kernel end (sp_mega.hpp).
 #ifdef SP_WAVE_PROF
 static __shared__ unsigned long long wprof_lds[16 * 8];
@@ -189,7 +190,7 @@ __device__ __forceinline__ void rng_prepare(Rng& r)
     const bool urgent = !r.ready && r.idx >= MT_N - RNG_MARGIN;
     if (__any(urgent)) {
         if (!r.ready) {
-            SP_WPROF(3, mt_twist_blocked<SP_TWIST_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r))));
+            mt_twist_blocked<SP_TWIST_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
             r.ready = 1;
         }
     }
@@ -1837,7 +1838,7 @@ __device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float
     ++c.shadow;
     ++c.rays;
     bool hit;
-    SP_WPROF(2, hit = scene_any(c.sc, r, tmin, tmax, c.st));
+    SP_WPROF(3, hit = scene_any(c.sc, r, tmin, tmax, c.st));
     return hit;
 }
 
@@ -2063,7 +2064,7 @@ __device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p,
     const float mmin = ray_offset(n, ms.dir);
     ++c.rays;
     LightHit lh;
-    SP_WPROF(2, lh = scene_intersect_lights(c.sc, mr, mmin, k_infinite, c.st));
+    SP_WPROF(3, lh = scene_intersect_lights(c.sc, mr, mmin, k_infinite, c.st));
     if (lh.hit) {
         if (!occluded(c, mr, mmin, k_infinite))
             Lr = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, light_hit_L(c.sc, lh, mr.d, c.q)), abs_f(dot(ms.dir, n))), w), ms.pdf));

@@ -21,7 +21,7 @@ tiles is rendered at the config's spp:
 Run in the build container (the reference sources are needed for oracle/_ref):
     python tests/golden/gen_full_scale.py            # both scenes
     python tests/golden/gen_full_scale.py --scene elf
-Outputs tests/golden/{lucy,elf}_full_tiles.npz.  lucy takes ~10 min of 8 cores (28.05 M
+Outputs tests/golden/{lucy,elf,spheres}_full_tiles.npz.  lucy takes ~10 min of 8 cores (28.05 M
 triangle parse + reference BVH build dominate), elf ~5 min.
 """
 from __future__ import annotations
@@ -49,6 +49,11 @@ CONFIGS = {
     "elf": dict(writer="write_elf_scene", kw=dict(n=290, max_depth=16), file="elf.sp",
                 mesh="stl_files/elf/nude-body_290.stl", w=4096, h=4096, spp=1024, integrator=5, probe_step=11,
                 picks=(10, 8, 8), seed=4),
+    # configs[1]: analytic spheres lit only by the 4096x2048 image-based environment light (the
+    # Distribution2D tables at twice the map resolution, 8192-entry CDFs); "mesh" is the map
+    "spheres": dict(writer="write_material_spheres_scene", kw={}, file="material_spheres_ibl.sp",
+                    mesh="clarens_night_02_4k.pfm", w=1024, h=1024, spp=64, integrator=6, probe_step=7,
+                    picks=(10, 8, 8), seed=5),
 }
 
 
@@ -105,12 +110,33 @@ def inside_mask(tile: int, w: int, h: int) -> np.ndarray:
     return (x0 + x < w) & (y0 + y < h)
 
 
-def pick_tiles(probe: np.ndarray, ids: np.ndarray, env: np.ndarray, w: int, h: int, picks, seed: int):
+def strip_blocks(text: str, block: str) -> str:
+    """The scene text without its top-level `block { ... }` entries (e.g. every sphere)."""
+    out, i = [], 0
+    lines = text.splitlines(keepends=True)
+    while i < len(lines):
+        if lines[i].strip() == block + " {":
+            depth = 0
+            while True:
+                depth += lines[i].count("{") - lines[i].count("}")
+                i += 1
+                if depth == 0:
+                    break
+            continue
+        out.append(lines[i])
+        i += 1
+    return "".join(out)
+
+
+def pick_tiles(probe: np.ndarray, ids: np.ndarray, env, w: int, h: int, picks, seed: int, env_probe=None):
     """Silhouette, high-contrast and random tiles from a 1-spp probe (see module docstring)."""
     rng = np.random.default_rng(seed)
     n_sil, n_con, n_rnd = picks
     full = np.array([inside_mask(int(t), w, h).all() for t in ids])
-    is_env = np.all(probe == env[None, None, :], axis=-1)  # camera ray escaped: L = the light's radiance
+    if env is None:  # image light: an escaped camera ray's radiance varies -- take pixels a spheres-free probe matches
+        is_env = np.zeros(probe.shape[:2], dtype=bool) if env_probe is None else np.all(probe == env_probe, axis=-1)
+    else:
+        is_env = np.all(probe == env[None, None, :], axis=-1)  # camera ray escaped: L = the light's radiance
     n_env = is_env.sum(axis=1)
     lum = probe @ np.array([0.2126, 0.7152, 0.0722], dtype=np.float32)
     contrast = lum.std(axis=1)
@@ -160,8 +186,21 @@ def generate(name: str, workdir: str, threads: int) -> str:
     probe_ids = np.arange(cfg["probe_step"] // 2, n_tiles, cfg["probe_step"], dtype=np.int32)
     probe = render(L, sc, integ, 1, probe_ids, threads)
     print(f"[{name}] probe: {probe_ids.size} tiles at 1 spp ({time.time() - t0:.0f} s)", flush=True)
-    env = np.array({"lucy": [1.0, 1.0, 1.3], "elf": [0.75, 0.75, 0.75]}[name], dtype=np.float32)
-    ids, kinds = pick_tiles(probe, probe_ids, env, w, h, cfg["picks"], cfg["seed"])
+    env, env_probe = None, None
+    if name == "spheres":
+        # the same probe with every sphere removed: pixels whose radiance it reproduces saw only the sky
+        bare = os.path.join(workdir, "material_spheres_sky_only.sp")
+        with open(path) as fh:
+            text = fh.read()
+        with open(bare, "w") as fh:
+            fh.write(strip_blocks(text, "sphere"))
+        sc0 = L.ref_scene_create(bare.encode(), w, h)
+        assert sc0, L.ref_last_error()
+        env_probe = render(L, sc0, integ, 1, probe_ids, threads)
+        L.ref_scene_free(sc0)
+    else:
+        env = np.array({"lucy": [1.0, 1.0, 1.3], "elf": [0.75, 0.75, 0.75]}[name], dtype=np.float32)
+    ids, kinds = pick_tiles(probe, probe_ids, env, w, h, cfg["picks"], cfg["seed"], env_probe)
     t1 = time.time()
     out = render(L, sc, integ, spp, ids, threads)
     print(f"[{name}] {ids.size} tiles at {spp} spp ({time.time() - t1:.0f} s)", flush=True)
@@ -181,13 +220,13 @@ def generate(name: str, workdir: str, threads: int) -> str:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scene", choices=["lucy", "elf", "all"], default="all")
+    ap.add_argument("--scene", choices=["lucy", "elf", "spheres", "all"], default="all")
     ap.add_argument("--workdir", default=os.path.join("/tmp", "sp_full_scale"))
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     a = ap.parse_args()
     if not os.path.exists(REF_LIB):
         sys.exit("oracle/_ref/libsp_ref.so is missing: run oracle/build_ref.sh (needs /root/reference)")
-    for name in (["elf", "lucy"] if a.scene == "all" else [a.scene]):
+    for name in (["spheres", "elf", "lucy"] if a.scene == "all" else [a.scene]):
         generate(name, a.workdir, a.threads)
 
 

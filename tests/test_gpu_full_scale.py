@@ -5,7 +5,11 @@ gen_full_scale.py renders them with oracle/_ref = the reference's sources).
   * lucy.sp: 28.05 M-triangle PLY stand-in, 1920x1080 @ 256 spp, DirectLighting -- 32 tiles
     (silhouettes, high-contrast drapery / floor contact, random);
   * elf.sp: 1.0 M-triangle binary STL stand-in, 4096x4096 @ 1024 spp, IterativeRRNEE with
-    max_depth 16 -- 26 tiles.
+    max_depth 16 -- 26 tiles;
+  * material_spheres.sp (configs[1]): analytic spheres lit only by the 4096x2048 image-based
+    environment light (Lights/Light.h:179 ImageBasedEnvironmentLight; math/Distribution2D.h:7
+    tables at twice the map resolution, 8192-entry CDFs), 1024x1024 @ 64 spp, DirectLighting --
+    26 tiles, with the guide-table lookup and with the replayed libstdc++ upper_bound.
 
 Bar (DESIGN.md "Parity chain"): bit-exact with the reference-order BVH (bvh_mode 1); with the SAH
 BVH rel-L2 < 1e-4 (north_star) and >= 99.9 % of pixels bit-exact.  Each test also asserts the BVH
@@ -115,3 +119,50 @@ def test_full_scale_lucy_every_pipeline(pipeline):
     out, st = sp.render_tiles(s, "direct_lighting", int(g["spp"]), ids, pipeline=pipeline)
     assert st.pipeline == sp.PIPELINES[pipeline]
     assert np.array_equal(out.view(np.uint32), g["radiance"].view(np.uint32)), rel_l2(out, g["radiance"])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("guide", ["1", "0"])
+@pytest.mark.parametrize("bvh", [1, 0])
+def test_full_scale_spheres_image_light(monkeypatch, bvh, guide):
+    # configs[1] at full size: the 4096x2048 map's Distribution2D (8192-entry marginal / conditional
+    # CDFs, the shifted, partly unsorted cdf the reference's normalisation leaves) sampled through
+    # the guide tables (SP_ENV_GUIDE=1, the default) and through the replayed upper_bound (0).
+    # Bit-exact with the reference-order BVH; the SAH BVH (3 nodes over 4 spheres) within the
+    # north-star tolerance.  Every pipeline AUTO may pick is covered: megakernel (the 1-GPU frame)
+    # and the sample chunks (image light: ck_count replays Light::sample).
+    monkeypatch.setenv("SP_ENV_GUIDE", guide)
+    g, s = full_scene("spheres")
+    s.upload(device=0, bvh_mode=bvh)
+    ids = g["tile_ids"].astype(np.int32)
+    ref = g["radiance"]
+    for pipeline in ("megakernel", "chunks"):
+        out, st = sp.render_tiles(s, "direct_lighting", int(g["spp"]), ids, pipeline=pipeline)
+        assert st.pipeline == sp.PIPELINES[pipeline] and st.samples == ids.size * 64 * int(g["spp"])
+        r = rel_l2(out, ref)
+        frac = float(np.mean(np.all(out == ref, axis=-1)))
+        print(f"spheres bvh={bvh} guide={guide} {pipeline}: rel_l2={r:.3e}, bit-exact pixels {frac:.5f}")
+        if bvh == 1:
+            assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), (r, frac)
+        else:
+            assert r < REL_L2_TOL and frac >= 0.999
+
+
+@pytest.mark.timeout(900)
+def test_full_scale_lucy_sah_megakernel():
+    # the pipeline that renders the 1-GPU lucy frame (configs[3] at N=1): the megakernel on the SAH
+    # BVH with the 8-wide any-hit BVH, against the reference's own tiles of the full 28 M-triangle
+    # scene (AUTO sends these 32 tiles to the sample chunks, so it is forced here)
+    g, s = full_scene("lucy")
+    s.upload(device=0, bvh_mode=0)
+    ids = g["tile_ids"].astype(np.int32)
+    ref = g["radiance"]
+    out, st = sp.render_tiles(s, "direct_lighting", int(g["spp"]), ids, pipeline="megakernel")
+    assert st.pipeline == sp.PIPELINES["megakernel"]
+    built = json.loads(str(g["bvh_sah"]))
+    assert st.stack_depth == built["stack_depth"]
+    r = rel_l2(out, ref)
+    frac = float(np.mean(np.all(out == ref, axis=-1)))
+    print(f"lucy SAH megakernel: rel_l2={r:.3e}, bit-exact pixels {frac:.5f}")
+    assert r < REL_L2_TOL
+    assert frac >= 0.999

@@ -6,7 +6,7 @@ import sys
 
 import numpy as np
 
-NAMES = ["sample (integrate)", "glossy rho estimate", "BVH / light queries", "MT twist (rng_prepare)"]
+NAMES = ["sample (integrate)", "glossy rho estimate", "closest-hit queries", "shadow / MIS queries"]
 
 
 def main(path):
@@ -16,8 +16,8 @@ def main(path):
         cyc, lane = v[2 * k], v[2 * k + 1]
         occ = lane / (64.0 * cyc) if cyc else 0.0
         print(f"{name:26s} wave-clocks {cyc:.4e}  share of sample {cyc / total:6.3f}  lane occupancy {occ:.3f}")
-    rest = v[0] - v[2] - v[4]
-    rest_l = v[1] - v[3] - v[5]
+    rest = v[0] - v[2] - v[4] - v[6]
+    rest_l = v[1] - v[3] - v[5] - v[7]
     print(f"{'rest of the sample':26s} wave-clocks {rest:.4e}  share of sample {rest / total:6.3f}  "
           f"lane occupancy {rest_l / (64.0 * rest) if rest else 0.0:.3f}")
 
