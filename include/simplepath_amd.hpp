@@ -100,8 +100,14 @@ public:
     }
     // HBM residency: bvh_mode 0 = SAH (fast), 1 = the reference's median split (bit-exact order).
     void upload(int device = 0, int bvh_mode = 0) const { check(sp_scene_upload(m_s, device, bvh_mode)); }
+    // ... with explicit accelerator options (sp_upload_params, ABI 4)
+    void upload(int device, const sp_upload_params& params) const { check(sp_scene_upload_ex(m_s, device, &params)); }
     sp_scene* handle() const noexcept { return m_s; }
 
+    // The reference's public Scene members (base/Scene.h:90-96), as read after loading.  They are
+    // snapshots for the host's own use: writing them does not change the render.  The image size
+    // is changed with set_resolution; max_depth / russian_roulette_depth / integrator come from
+    // the scene file (render with another integrator through Integrator).
     int            image_width            = 0;
     int            image_height           = 0;
     int            russian_roulette_depth = 3;

@@ -17,7 +17,8 @@
  *                                         russian_roulette_depth, max_depth, integrator_type)
  *   sp_scene_get_desc                     the primitive / light / material / camera state
  *                                         held by base/Scene.h:99-105 (flattened, host memory)
- *   sp_scene_upload                       (no reference counterpart: HBM residency)
+ *   sp_scene_upload / sp_scene_upload_ex  (no reference counterpart: HBM residency; the
+ *                                         Scene ctor's accelerator build, base/Scene.h:59)
  *   sp_scene_bvh_build_info               base/Scene.h:59 Scene ctor's BVHAccelerator build
  *                                         (shapes/BVHAccelerator.h:173), host only: statistics
  *   sp_render_tiles                       main.cpp:77-107 `render_thread`: for each scheduled
@@ -44,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 3
+#define SP_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------------- */
 enum {
@@ -177,14 +178,33 @@ typedef struct sp_scene_desc {
 
 /* ---- render ------------------------------------------------------------------------ */
 
+/* Zero-initialise (`sp_render_params p = {0};`): every field added in a later ABI means
+ * "automatic" at 0.  Stream order: with stats == NULL, no SP_RENDER_STAGE_TIMING flag and the
+ * tile list on the device (d_tile_ids) or absent, sp_render_tiles only enqueues work on `stream`
+ * and returns -- two calls and a dependent kernel can be queued back to back with no host wait.
+ * Requesting stats waits for the render (the counters are read back).  Calls on one scene share
+ * its device scratch, so they must be ordered on one stream (or the host must wait in between). */
 typedef struct sp_render_params {
     int32_t        integrator;        /* SP_INTEGRATOR_*; 0 => scene's (DirectLighting if unset: main.cpp:387-392) */
     uint32_t       samples_per_pixel; /* main.cpp `--samples`                                    */
-    const int32_t* tile_ids;          /* host array of tile indices (ColumnMajor order); NULL => all tiles */
-    int64_t        num_tiles;         /* length of tile_ids (ignored when tile_ids == NULL)      */
+    const int32_t* tile_ids;          /* host array of tile indices (ColumnMajor order); NULL => d_tile_ids or all tiles */
+    int64_t        num_tiles;         /* length of tile_ids / d_tile_ids (ignored when both are NULL) */
     void*          stream;            /* hipStream_t, NULL = default stream                      */
-    int32_t        bvh_mode;          /* 0 = SAH (fast), 1 = reference median-split order        */
-    int32_t        flags;             /* SP_PIPELINE_* (0 = automatic)                            */
+    int32_t        bvh_mode;          /* unused: the BVH is chosen at upload (kept for layout)     */
+    int32_t        flags;             /* SP_PIPELINE_* (0 = automatic) | SP_RENDER_STAGE_TIMING   */
+    /* ---- ABI 4 ---- */
+    const int32_t* d_tile_ids;        /* DEVICE array of num_tiles tile indices, used when tile_ids is
+                                         NULL: not copied or checked on the host (an id outside the
+                                         image renders as zeros)                                  */
+    int32_t        waves_per_simd;    /* megakernel occupancy (__launch_bounds__ variant): 0 = automatic
+                                         (DirectLighting 4, IterativeRRNEE 3, fewer if the LDS caps it);
+                                         else DirectLighting 1-4, IterativeRRNEE 2-4               */
+    int32_t        chunks_per_pixel;  /* sample-chunk pipeline: 0 = automatic (~120K (tile, chunk) items),
+                                         else 1..samples_per_pixel                                 */
+    float          chunk_max_gb;      /* sample-chunk buffer budget in GB: 0 = 96, never more than the
+                                         device's free memory; AUTO falls back to the megakernel when
+                                         the buffers do not fit                                    */
+    int32_t        reserved[3];       /* must be 0                                                  */
 } sp_render_params;
 
 /* Device pipeline selection (sp_render_params.flags).  All produce identical images. */
@@ -192,13 +212,27 @@ enum {
     SP_PIPELINE_AUTO       = 0, /* by work size: megakernel, or sample chunks for DirectLighting
                                    below 24000 tiles when their buffers fit     */
     SP_PIPELINE_MEGAKERNEL = 1, /* one lane owns one pixel for all samples (sp_mega.hpp)        */
-    SP_PIPELINE_WAVEFRONT  = 2, /* DirectLighting: per-sample primary/shade/shadow kernels       */
+    SP_PIPELINE_WAVEFRONT  = 2, /* DirectLighting: per-sample primary/shade/shadow kernels with
+                                   ballot/prefix-sum shadow-ray compaction (sp_wave.hip)         */
     SP_PIPELINE_SAMPLE_CHUNKS = 3, /* DirectLighting: each pixel's samples in parallel chunks
                                       (stream state snapshots; sp_chunk.hip)                      */
-                                /* (sp_wave.hip); BruteForceIterative(RR), IterativeRRNEE:      */
-                                /* trace/shade rounds over refilled tile slots (sp_wpath.hip)   */
-    SP_RENDER_STAGE_TIMING = 4  /* flag: HIP events between launches fill sp_render_stats.stage_ms */
+    SP_RENDER_STAGE_TIMING = 4  /* flag: HIP events between launches fill sp_render_stats.stage_ms
+                                   (waits for the render)                                          */
 };
+
+/* Accelerator options of sp_scene_upload_ex (ABI 4).  Zero-initialise: 0 = automatic. */
+enum { SP_WALK_AUTO = 0, SP_WALK_STACKLESS = 1 };
+typedef struct sp_upload_params {
+    int32_t bvh_mode;         /* 0 = SAH (fast), 1 = reference median-split order (tie-exact)       */
+    int32_t walk;             /* SP_WALK_AUTO: per-wave LDS stack unless the BVH is deeper than
+                                 stack_max_levels; SP_WALK_STACKLESS: parent links always         */
+    int32_t stack_max_levels; /* 0 = 96                                                            */
+    int32_t no_wide_bvh;      /* 1: any-hit queries walk the binary BVH instead of the 8-wide one   */
+    int32_t env_replay;       /* 1: image-light CDF lookups replay libstdc++ upper_bound step by step
+                                 instead of the guide tables (identical results)                    */
+    int32_t sah_leaf;         /* SAH leaf size 1-4: 0 = 4                                          */
+    int32_t reserved[2];      /* must be 0                                                          */
+} sp_upload_params;
 
 typedef struct sp_render_stats {
     uint64_t rays;            /* every ray cast: camera/extension + shadow + MIS rays            */
@@ -253,6 +287,11 @@ int  sp_tile_origin(int32_t width, int32_t height, int64_t tile, int32_t* x0, in
 /* Device side. */
 int  sp_device_count(int32_t* out);
 int  sp_scene_upload(sp_scene* scene, int32_t device, int32_t bvh_mode);
+/* sp_scene_upload with explicit accelerator options (NULL = all automatic with bvh_mode 0).  A
+ * scene already resident on `device` with the same effective options is not re-uploaded.  The
+ * SP_STACKLESS / SP_STACK_MAX / SP_WIDE / SP_ENV_GUIDE / SP_SAH_LEAF environment variables
+ * override fields left automatic (test hooks). */
+int  sp_scene_upload_ex(sp_scene* scene, int32_t device, const sp_upload_params* params);
 /* Render tiles into a DEVICE buffer laid out tile-packed: out[(slot*64 + morton)*3 + c],
  * slot = position of the tile in params->tile_ids (or the tile index itself when NULL).
  * Pixels of clipped border tiles that fall outside the image are written as 0. */

@@ -113,9 +113,20 @@ class Scene:
     def set_resolution(self, width: int, height: int) -> None:
         check(lib().sp_scene_set_resolution(self._h, width, height))
 
-    def upload(self, device: int = 0, bvh_mode: int = 0) -> None:
-        """bvh_mode 0 = SAH (throughput), 1 = the reference's median-split BVH (tie-exact order)."""
-        check(lib().sp_scene_upload(self._h, device, bvh_mode))
+    def upload(self, device: int = 0, bvh_mode: int = 0, stackless: bool = False, stack_max_levels: int = 0,
+               wide_bvh: bool = True, env_replay: bool = False, sah_leaf: int = 0) -> None:
+        """bvh_mode 0 = SAH (throughput), 1 = the reference's median-split BVH (tie-exact order).
+        The other options (sp_upload_params) change how the same image is computed, never the
+        image: the parent-link walk, the LDS-stack depth budget, the 8-wide any-hit BVH, the
+        image-light guide tables, the SAH leaf size."""
+        p = _abi.sp_upload_params()
+        p.bvh_mode = bvh_mode
+        p.walk = _abi.SP_WALK_STACKLESS if stackless else _abi.SP_WALK_AUTO
+        p.stack_max_levels = stack_max_levels
+        p.no_wide_bvh = 0 if wide_bvh else 1
+        p.env_replay = 1 if env_replay else 0
+        p.sah_leaf = sah_leaf
+        check(lib().sp_scene_upload_ex(self._h, device, C.byref(p)))
         self._device = device
 
     def bvh_info(self):
@@ -174,7 +185,7 @@ STAGE_TIMING = 4  # SP_RENDER_STAGE_TIMING
 
 
 def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeline="auto",
-            stage_timing=False) -> tuple:
+            stage_timing=False, waves_per_simd=0, chunks_per_pixel=0, chunk_max_gb=0.0) -> tuple:
     if isinstance(integrator, str):
         integrator = string_to_integrator_type(integrator)
     p = _abi.sp_render_params()
@@ -187,6 +198,9 @@ def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeli
         p.num_tiles = keep.size
     p.stream = stream
     p.flags = (PIPELINES[pipeline] if isinstance(pipeline, str) else int(pipeline)) | (STAGE_TIMING if stage_timing else 0)
+    p.waves_per_simd = int(waves_per_simd)
+    p.chunks_per_pixel = int(chunks_per_pixel)
+    p.chunk_max_gb = float(chunk_max_gb)
     return p, keep
 
 
@@ -196,10 +210,11 @@ def _stats(s: _abi.sp_render_stats) -> RenderStats:
 
 
 def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Optional[Sequence[int]] = None,
-                 pipeline="auto"):
-    """Render tiles on the GPU; returns (tile-packed radiance [n,64,3] float32, RenderStats)."""
+                 pipeline="auto", **options):
+    """Render tiles on the GPU; returns (tile-packed radiance [n,64,3] float32, RenderStats).
+    options: waves_per_simd, chunks_per_pixel, chunk_max_gb (sp_render_params, ABI 4)."""
     p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids),
-                      pipeline=pipeline)
+                      pipeline=pipeline, **options)
     n = keep.size if keep is not None else TileScheduler(scene.width, scene.height).get_num_tiles()
     out = np.zeros((max(n, 1), 64, 3), dtype=np.float32)
     st = _abi.sp_render_stats()
@@ -208,10 +223,20 @@ def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Opt
 
 
 def render_tiles_device(scene: Scene, integrator, num_pixel_samples: int, tile_ids, out_ptr: int, stream=None,
-                        pipeline="auto", stage_timing=False):
-    """Render into a caller-owned device buffer (e.g. a torch.cuda tensor's data_ptr())."""
+                        pipeline="auto", stage_timing=False, stats=True, d_tile_ids: int = 0,
+                        num_tiles: int = 0, **options):
+    """Render into a caller-owned device buffer (e.g. a torch.cuda tensor's data_ptr()).
+    tile_ids: host tile list (None: d_tile_ids, a device pointer to num_tiles int32 ids, or every
+    tile).  With stats=False (and no stage timing, no host tile list) the render is only enqueued
+    on `stream`: the call returns without waiting (returns None)."""
     p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids), stream,
-                      pipeline, stage_timing)
+                      pipeline, stage_timing, **options)
+    if d_tile_ids:
+        p.d_tile_ids = C.c_void_p(d_tile_ids)
+        p.num_tiles = int(num_tiles)
+    if not stats:
+        check(lib().sp_render_tiles(scene.handle, C.byref(p), C.c_void_p(out_ptr), None))
+        return None
     st = _abi.sp_render_stats()
     check(lib().sp_render_tiles(scene.handle, C.byref(p), C.c_void_p(out_ptr), C.byref(st)))
     return _stats(st)

@@ -92,7 +92,19 @@ class sp_render_params(C.Structure):
         ("integrator", C.c_int32), ("samples_per_pixel", C.c_uint32),
         ("tile_ids", C.POINTER(C.c_int32)), ("num_tiles", C.c_int64),
         ("stream", C.c_void_p), ("bvh_mode", C.c_int32), ("flags", C.c_int32),
+        # ABI 4
+        ("d_tile_ids", C.c_void_p), ("waves_per_simd", C.c_int32), ("chunks_per_pixel", C.c_int32),
+        ("chunk_max_gb", C.c_float), ("reserved", C.c_int32 * 3),
     ]
+
+
+SP_WALK_AUTO, SP_WALK_STACKLESS = 0, 1
+
+
+class sp_upload_params(C.Structure):
+    _fields_ = [("bvh_mode", C.c_int32), ("walk", C.c_int32), ("stack_max_levels", C.c_int32),
+                ("no_wide_bvh", C.c_int32), ("env_replay", C.c_int32), ("sah_leaf", C.c_int32),
+                ("reserved", C.c_int32 * 2)]
 
 
 class sp_render_stats(C.Structure):
@@ -123,6 +135,7 @@ SIGNATURES = {
     "sp_tile_origin": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "sp_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "sp_scene_upload": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "sp_scene_upload_ex": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(sp_upload_params)]),
     "sp_render_tiles": (C.c_int, [C.c_void_p, C.POINTER(sp_render_params), C.c_void_p, C.POINTER(sp_render_stats)]),
     "sp_render_tiles_host": (C.c_int, [C.c_void_p, C.POINTER(sp_render_params), C.POINTER(C.c_float),
                                        C.POINTER(sp_render_stats)]),

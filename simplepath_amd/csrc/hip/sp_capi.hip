@@ -19,8 +19,6 @@ namespace spd {
 hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
-hipError_t launch_tile_cost(const Scene& sc, const int32_t* tile_ids, int64_t n_tiles, int32_t tiles_x, float* cost,
-                            hipStream_t stream);
 } // namespace spd
 
 namespace {
@@ -95,10 +93,53 @@ sph::PrimBounds sphere_bounds(const spm::aff& o2w)
     return b;
 }
 
+// Accelerator options of an upload (sp_upload_params, ABI 4): explicit fields win; fields left
+// automatic take the SP_* environment overrides (test hooks), else the measured defaults.
+struct UploadOpts {
+    int  bvh_mode   = 0;
+    bool stackless  = false; // forced parent-link walk
+    int  stack_max  = 96;    // deepest BVH (levels) walked with the LDS stack
+    bool wide       = true;  // 8-wide any-hit BVH on SAH scenes
+    bool env_guide  = true;  // image-light guide tables
+    int  sah_leaf   = 4;
+    bool operator==(const UploadOpts& o) const
+    {
+        return bvh_mode == o.bvh_mode && stackless == o.stackless && stack_max == o.stack_max && wide == o.wide &&
+               env_guide == o.env_guide && sah_leaf == o.sah_leaf;
+    }
+};
+
+static int env_int(const char* name, int fallback)
+{
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : fallback;
+}
+
+int resolve_upload(const sp_upload_params* p, UploadOpts& o)
+{
+    const sp_upload_params z{};
+    if (!p) p = &z;
+    for (int32_t r : p->reserved)
+        if (r != 0) return fail(SP_ERR_ARG, "sp_upload_params.reserved must be 0");
+    if (p->bvh_mode != 0 && p->bvh_mode != 1) return fail(SP_ERR_ARG, "bvh_mode must be 0 (SAH) or 1 (reference)");
+    if (p->walk != SP_WALK_AUTO && p->walk != SP_WALK_STACKLESS) return fail(SP_ERR_ARG, "walk must be SP_WALK_AUTO or SP_WALK_STACKLESS");
+    if (p->stack_max_levels < 0) return fail(SP_ERR_ARG, "stack_max_levels < 0");
+    if (p->sah_leaf < 0 || p->sah_leaf > 4) return fail(SP_ERR_ARG, "sah_leaf must be 0 (automatic) or 1..4");
+    o.bvh_mode  = p->bvh_mode;
+    o.stackless = p->walk == SP_WALK_STACKLESS || (p->walk == SP_WALK_AUTO && env_int("SP_STACKLESS", 0) != 0);
+    o.stack_max = p->stack_max_levels ? p->stack_max_levels : std::max(1, env_int("SP_STACK_MAX", 96));
+    o.wide      = !p->no_wide_bvh && env_int("SP_WIDE", 1) != 0;
+    o.env_guide = !p->env_replay && env_int("SP_ENV_GUIDE", 1) != 0;
+    // SAH leaf size limit (1..4: 8 collapsed leaves of a wide node must fit its 5-bit leaf
+    // offsets; the sweep in DESIGN.md §4 found 4 best)
+    o.sah_leaf  = p->sah_leaf ? p->sah_leaf : std::max(1, std::min(4, env_int("SP_SAH_LEAF", 4)));
+    return SP_OK;
+}
+
 // Scene ctor partition (base/Scene.h:29: bounded primitives first, planes after, libstdc++
 // std::partition order) and the BVH over the bounded part: the reference's median split
 // (bvh_mode 1, shapes/BVHAccelerator.h:173) or SAH.
-sph::Bvh geometry_bvh(const sph::Scene& h, int bvh_mode, std::vector<int32_t>& prims, size_t& part)
+sph::Bvh geometry_bvh(const sph::Scene& h, const UploadOpts& o, std::vector<int32_t>& prims, size_t& part)
 {
     prims.resize(h.prim_kind.size());
     for (size_t i = 0; i < prims.size(); ++i) prims[i] = (int32_t)i;
@@ -110,32 +151,16 @@ sph::Bvh geometry_bvh(const sph::Scene& h, int bvh_mode, std::vector<int32_t>& p
         if (h.prim_kind[p] == SP_PRIM_TRIANGLE) bounds.push_back(tri_bounds(h, h.prim_index[p]));
         else bounds.push_back(sphere_bounds(from_desc(h.shapes[h.prim_index[p]].object_to_world)));
     }
-    // SAH leaf size limit (SP_SAH_LEAF tuning knob, 1..4: 8 collapsed leaves of a wide node must
-    // fit its 5-bit leaf offsets; the sweep in DESIGN.md §4 found 4 best)
-    int sah_leaf = 4;
-    if (const char* v = std::getenv("SP_SAH_LEAF")) sah_leaf = std::max(1, std::min(4, std::atoi(v)));
-    return (bvh_mode == 1) ? sph::build_bvh_reference(bounds) : sph::build_bvh_sah(bounds, sah_leaf);
+    return (o.bvh_mode == 1) ? sph::build_bvh_reference(bounds) : sph::build_bvh_sah(bounds, o.sah_leaf);
 }
 
-// SAH scenes get the 8-wide quantised BVH for any-hit queries (SP_WIDE=0 keeps the binary walk)
-bool wide_enabled(int bvh_mode)
-{
-    const char* v = std::getenv("SP_WIDE");
-    return bvh_mode != 1 && (v ? std::atoi(v) != 0 : true);
-}
+// SAH scenes get the 8-wide quantised BVH for any-hit queries (no_wide_bvh keeps the binary walk)
+bool wide_enabled(const UploadOpts& o) { return o.bvh_mode != 1 && o.wide; }
 
-// Traversal-stack budget: a BVH deeper than this many levels is walked without a stack (parent
-// links, sp_path.hpp bvh_next) instead of failing.  96 entries x 4 B x 64 lanes x 4 waves = 96 KB
-// of LDS, which leaves room for the 16 KB RSQRTSS table and a second block per CU.
-// SP_STACKLESS=1 forces the stackless walk (tests), SP_STACK_MAX=<levels> moves the threshold.
-bool stackless_for(int depth)
-{
-    if (const char* v = std::getenv("SP_STACKLESS"))
-        if (std::atoi(v) != 0) return true;
-    int max_levels = 96;
-    if (const char* v = std::getenv("SP_STACK_MAX")) max_levels = std::max(1, std::atoi(v));
-    return depth + 1 > max_levels;
-}
+// Traversal-stack budget: a BVH deeper than stack_max levels (default 96) is walked without a
+// stack (parent links, sp_path.hpp bvh_next) instead of failing.  96 entries x 4 B x 64 lanes x 4
+// waves = 96 KB of LDS, which leaves room for the 16 KB RSQRTSS table and a second block per CU.
+bool stackless_for(const UploadOpts& o, int depth) { return o.stackless || depth + 1 > o.stack_max; }
 
 // Scene ctor's light accelerator (base/Scene.h:29): sphere lights first (libstdc++
 // std::partition order), the reference BVH over them; the rest are unbounded
@@ -175,6 +200,7 @@ struct sp_scene {
     // device residency
     int                  device   = -1;
     int                  bvh_mode = -1;
+    UploadOpts           opts{};    // effective accelerator options of the resident upload
     std::vector<DevBuf>  bufs;
     spd::Scene           dev{};
     int                  geom_depth = 0, light_depth = 0;
@@ -197,17 +223,8 @@ struct sp_scene {
     void*                ck_buf     = nullptr; // sample-chunk pipeline: hits, radiance, snapshots
     size_t               ck_cap     = 0;
     int32_t*             ck_ctr     = nullptr;
-    float*               d_cost     = nullptr; // megakernel tile order (longest first)
-    int32_t*             d_order    = nullptr;
-    size_t               order_cap  = 0;
     void*                deep_buf   = nullptr; // recursive integrators beyond MAX_RECURSION levels
     size_t               deep_cap   = 0;
-    // multi-bounce wavefront (sp_wpath.hip)
-    void*                wp_buf     = nullptr;
-    size_t               wp_cap     = 0;
-    int32_t*             wp_ctl     = nullptr; // device int32[2]
-    int32_t*             wp_host    = nullptr; // pinned int32[2]
-    hipEvent_t           wp_ev[2]   = { nullptr, nullptr };
 
     void release()
     {
@@ -239,20 +256,11 @@ struct sp_scene {
         ev_fork = nullptr;
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
-        if (wp_buf) (void)hipFree(wp_buf);
         if (deep_buf) (void)hipFree(deep_buf);
         if (ck_buf) (void)hipFree(ck_buf);
         if (ck_ctr) (void)hipFree(ck_ctr);
         ck_buf = nullptr; ck_ctr = nullptr; ck_cap = 0;
-        if (d_cost) (void)hipFree(d_cost);
-        if (d_order) (void)hipFree(d_order);
-        d_cost = nullptr; d_order = nullptr; order_cap = 0;
         deep_buf = nullptr; deep_cap = 0;
-        if (wp_ctl) (void)hipFree(wp_ctl);
-        if (wp_host) (void)hipHostFree(wp_host);
-        for (auto& e : wp_ev)
-            if (e) (void)hipEventDestroy(e);
-        wp_buf = nullptr; wp_cap = 0; wp_ctl = nullptr; wp_host = nullptr; wp_ev[0] = wp_ev[1] = nullptr;
         mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
         ev0 = ev1 = nullptr;
         mt_waves = 0; d_tiles_cap = 0;
@@ -582,18 +590,21 @@ float sp_host_rsqrt_emulated(float x)
     return spm::rsqrtss_emulated(x, t);
 }
 
-static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
+static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params* up_params)
 {
     if (!s) return fail(SP_ERR_ARG, "null scene");
-    if (bvh_mode != 0 && bvh_mode != 1) return fail(SP_ERR_ARG, "bvh_mode must be 0 (SAH) or 1 (reference)");
+    UploadOpts opts;
+    if (int rc0 = resolve_upload(up_params, opts)) return rc0;
+    const int bvh_mode = opts.bvh_mode;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SP_ERR_HIP, "no HIP device");
     if (device < 0 || device >= ndev) return fail(SP_ERR_ARG, "device out of range");
-    if (s->device == device && s->bvh_mode == bvh_mode) return SP_OK;
+    if (s->device == device && s->opts == opts) return SP_OK;
     s->release();
     SP_HIP(hipSetDevice(device));
     s->device   = device;
     s->bvh_mode = bvh_mode;
+    s->opts     = opts;
     const sph::Scene& h = *s->host;
     spd::Scene&       d = s->dev;
     d                   = spd::Scene{};
@@ -624,7 +635,7 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
     // ---- geometry: Scene ctor partition (base/Scene.h:29) then BVH over the bounded part
     std::vector<int32_t> prims;
     size_t               part = 0;
-    const sph::Bvh       bvh  = geometry_bvh(h, bvh_mode, prims, part);
+    const sph::Bvh       bvh  = geometry_bvh(h, opts, prims, part);
     std::vector<spd::Shape> shapes;
     for (auto& sh : h.shapes) {
         spd::Shape x{};
@@ -680,10 +691,10 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
 
     // SAH: 8-wide quantised BVH for any-hit queries (SP_WIDE=0 keeps the binary walk); a
     // stackless scene walks the binary BVH only
-    const bool          stackless = stackless_for(std::max(bvh.max_depth, lbvh.max_depth));
+    const bool          stackless = stackless_for(opts, std::max(bvh.max_depth, lbvh.max_depth));
     sph::WideBvh        wide;
     std::vector<float4> wslot_tri;
-    if (wide_enabled(bvh_mode) && !nodes.empty() && !stackless) {
+    if (wide_enabled(opts) && !nodes.empty() && !stackless) {
         wide = sph::build_wide(bvh);
         wslot_tri.resize(wide.slot_of.size() * 3);
         for (size_t i = 0; i < wide.slot_of.size(); ++i)
@@ -750,8 +761,7 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
         x.marg_guide = nullptr;
         x.cond_bits  = m.cond_bits;
         x.marg_bits  = m.marg_bits;
-        const char* ge = std::getenv("SP_ENV_GUIDE"); // 0: replay the exact upper_bound (comparison)
-        if (m.guided && !(ge && std::atoi(ge) == 0)) {
+        if (m.guided && opts.env_guide) { // else the exact upper_bound replay (identical results)
             up(m.cond_guide, &x.cond_guide);
             up(m.marg_guide, &x.marg_guide);
         }
@@ -821,15 +831,22 @@ static int scene_upload_impl(sp_scene* s, int32_t device, int32_t bvh_mode)
 
 // No C++ exception crosses the C ABI: host-side failures (allocation, BVH encoding limits)
 // come back as error codes with sp_last_error() set.
-int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
+int sp_scene_upload_ex(sp_scene* s, int32_t device, const sp_upload_params* params)
 {
     try {
-        return scene_upload_impl(s, device, bvh_mode);
+        return scene_upload_impl(s, device, params);
     } catch (const sph::SpError& e) {
         return fail(e.code, e.what());
     } catch (const std::exception& e) {
         return fail(SP_ERR_UNSUPPORTED, std::string("scene upload failed: ") + e.what());
     }
+}
+
+int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
+{
+    sp_upload_params p{};
+    p.bvh_mode = bvh_mode;
+    return sp_scene_upload_ex(s, device, &p);
 }
 
 static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats);
@@ -844,19 +861,74 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     }
 }
 
+// Sample-chunk buffer plan (sp_chunk.hip): the same sizes decide AUTO and are allocated.
+struct ChunkPlan {
+    int64_t  chunks = 1;    // chunks per pixel
+    uint32_t len = 1;       // samples per chunk (the last may be short)
+    uint32_t gens = 0;      // generator-store generations per pixel
+    bool     known_draws = true;
+    size_t   b_hits = 0, b_L = 0, b_snap = 0, b_ctl = 0, b_draws = 0, total = 0;
+};
+static ChunkPlan chunk_plan(const sp_scene* s, int64_t n_tiles, uint32_t spp, int64_t chunks_req)
+{
+    ChunkPlan c;
+    // chunks per pixel: the smallest power of two (<= 32) giving ~120K (tile, chunk) items (the
+    // best of the bunny 2/4/8-way shard sweep) unless the caller asks for a count
+    c.chunks = 1;
+    while (c.chunks < 32 && n_tiles * c.chunks < 120000) c.chunks *= 2;
+    if (chunks_req > 0) c.chunks = chunks_req;
+    c.chunks = std::min<int64_t>(c.chunks, spp);
+    c.len    = (uint32_t)((spp + c.chunks - 1) / c.chunks);
+    c.chunks = (spp + c.len - 1) / c.len;
+    // a DirectLighting sample draws at most 34 words per light (Light::sample 2 + glossy rho 32);
+    // +2 generations for the first twist and the one rng_prepare may twist ahead
+    const uint64_t max_draws = (uint64_t)spp * (uint64_t)std::max(1, s->dev.n_lights) * 34;
+    c.gens = (uint32_t)((max_draws + spm::MT_N - 1) / spm::MT_N + 2);
+    // per-sample draw counts from the camera pass unless an image light makes them depend on the
+    // drawn numbers (then ck_count replays Light::sample); SP_CHUNK_REPLAY=1 forces the replay (test)
+    c.known_draws = s->dev.n_lights <= 1000;
+    for (const auto& l : s->host->lights)
+        if (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) c.known_draws = false;
+    if (const char* v = std::getenv("SP_CHUNK_REPLAY")) c.known_draws = c.known_draws && std::atoi(v) == 0;
+    const size_t n_px = (size_t)n_tiles * 64;
+    c.b_hits  = n_px * spp * 16;
+    c.b_L     = n_px * spp * 12;
+    c.b_snap  = (size_t)n_tiles * c.gens * spm::MT_N * 64 * 8;
+    c.b_ctl   = (size_t)c.chunks * n_px * 4;
+    c.b_draws = c.known_draws ? n_px * spp * 2 : 0;
+    c.total   = c.b_hits + c.b_L + c.b_snap + c.b_ctl + c.b_draws + 4 * 256;
+    return c;
+}
+
 static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats)
 {
     if (!s || !p || !d_out) return fail(SP_ERR_ARG, "null argument");
     if (s->device < 0) return fail(SP_ERR_STATE, "sp_scene_upload must be called before sp_render_tiles");
     if (p->samples_per_pixel == 0) return fail(SP_ERR_ARG, "samples_per_pixel must be > 0");
+    for (int32_t r : p->reserved)
+        if (r != 0) return fail(SP_ERR_ARG, "sp_render_params.reserved must be 0");
+    if (p->tile_ids && p->d_tile_ids) return fail(SP_ERR_ARG, "give tile_ids (host) or d_tile_ids (device), not both");
+    if (p->chunks_per_pixel < 0) return fail(SP_ERR_ARG, "chunks_per_pixel < 0");
+    if (!(p->chunk_max_gb >= 0.0f)) return fail(SP_ERR_ARG, "chunk_max_gb < 0");
+    if ((p->flags & ~(3 | SP_RENDER_STAGE_TIMING)) != 0) return fail(SP_ERR_ARG, "unknown flags");
     SP_HIP(hipSetDevice(s->device));
     int32_t integ = p->integrator;
     if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = s->host->integrator;
     if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = SP_INTEGRATOR_DIRECT_LIGHTING; // main.cpp:390
     if (integ < SP_INTEGRATOR_MANDELBROT || integ > SP_INTEGRATOR_WHITTED) return fail(SP_ERR_ARG, "Unknown integrator type");
+    // megakernel occupancy request: DirectLighting 1..4 waves per SIMD, IterativeRRNEE 2..4;
+    // the other integrators have one variant each (0 = automatic)
+    const int waves_req = p->waves_per_simd;
+    if (waves_req != 0) {
+        const bool ok = integ == SP_INTEGRATOR_DIRECT_LIGHTING ? (waves_req >= 1 && waves_req <= 4)
+                        : integ == SP_INTEGRATOR_ITERATIVE_RRNEE ? (waves_req >= 2 && waves_req <= 4)
+                                                                  : false;
+        if (!ok) return fail(SP_ERR_ARG, "waves_per_simd: DirectLighting 1-4, IterativeRRNEE 2-4, else 0");
+    }
     int64_t total;
     sp_tile_count(s->dev.width, s->dev.height, &total);
-    const int64_t n_tiles = p->tile_ids ? p->num_tiles : total;
+    const bool    listed  = p->tile_ids || p->d_tile_ids;
+    const int64_t n_tiles = listed ? p->num_tiles : total;
     if (n_tiles < 0) return fail(SP_ERR_ARG, "num_tiles < 0");
     if (p->tile_ids)
         for (int64_t i = 0; i < n_tiles; ++i)
@@ -864,6 +936,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     hipStream_t stream = static_cast<hipStream_t>(p->stream);
     if (stats) *stats = sp_render_stats{};
     if (n_tiles == 0) return SP_OK;
+    const int32_t* d_ids = p->d_tile_ids; // device tile list (nullptr: slot = tile)
     if (p->tile_ids) {
         if ((size_t)n_tiles > s->d_tiles_cap) {
             if (s->d_tiles) (void)hipFree(s->d_tiles);
@@ -872,6 +945,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             s->d_tiles_cap = (size_t)n_tiles;
         }
         SP_HIP(hipMemcpyAsync(s->d_tiles, p->tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+        d_ids = s->d_tiles;
     }
     if (s->n_cu == 0) {
         hipDeviceProp_t prop;
@@ -880,102 +954,65 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     }
     const bool timing   = (p->flags & SP_RENDER_STAGE_TIMING) != 0;
     float      stage[4] = { 0, 0, 0, 0 };
-    int pipeline = p->flags & 3;
+    const int  asked    = p->flags & 3;
+    int        pipeline = asked;
     if (pipeline == SP_PIPELINE_SAMPLE_CHUNKS && integ != SP_INTEGRATOR_DIRECT_LIGHTING)
         return fail(SP_ERR_UNSUPPORTED, "the sample-chunk pipeline implements DirectLighting");
-    const bool wave_ok  = integ == SP_INTEGRATOR_DIRECT_LIGHTING && s->dev.n_lights <= spd::WF_MAX_LIGHTS;
-    const bool wpath_ok = spd::wpath_supports(integ);
-    if (pipeline == SP_PIPELINE_WAVEFRONT && !wave_ok && !wpath_ok)
-        return fail(SP_ERR_UNSUPPORTED, "wavefront pipeline supports DirectLighting (<= 32 lights), "
-                                        "BruteForceIterative(RR) and IterativeRRNEE");
-    // AUTO: the split pipeline where it wins -- DirectLighting; the iterative integrators run the
-    // regenerating megakernel (sp_mega.hpp), which measured faster than sp_wpath
-    // DirectLighting: the wavefront needs many pixels in flight -- every launch waits for its
-    // slowest wave, once per sample.  Below SP_WAVE_MIN_TILES tiles (default 24000: between
-    // the 1-GPU frame, 32400 tiles, and its 2-GPU shard, 16200) the persistent megakernel,
-    // with its tiles taken longest-first, is faster.
-    // Below SP_CHUNK_MAX_TILES (default 12000: between the 2- and 4-GPU shards) even the
-    // megakernel waits on single pixels' sample chains; the sample-chunk pipeline splits them
-    // (4-GPU shard 1285 -> 1490, 8-GPU shard 823 -> 1384 Mrays/s).
-    // Round 2, device code without SLP vectorisation (profiles/r02/s5): the megakernel at 4 waves per
-    // SIMD renders the 1-GPU frame at 2706 Mrays/s against 2305 for the wavefront, and the sample
-    // chunks the 2-way shard at 2507 against 2138: AUTO now uses the wavefront only from
-    // SP_WAVE_MIN_TILES (default: never) and the chunks below SP_CHUNK_MAX_TILES = 24000.
+    const bool wave_ok = integ == SP_INTEGRATOR_DIRECT_LIGHTING && s->dev.n_lights <= spd::WF_MAX_LIGHTS;
+    if (pipeline == SP_PIPELINE_WAVEFRONT && !wave_ok)
+        return fail(SP_ERR_UNSUPPORTED, "the wavefront pipeline implements DirectLighting (<= 32 lights)");
+    // AUTO (measurements: DESIGN.md §3, §6).  The megakernel renders the 1-GPU frame fastest
+    // (bunny 1080p @ 256 spp: 2974 Mrays/s, wavefront 2305).  Below SP_CHUNK_MAX_TILES = 24000
+    // tiles (the 2-8-GPU shards) one pixel's sample chain bounds the megakernel and the sample
+    // chunks win (8-way shard 2444 against 823), when their buffers fit the budget.  With an image
+    // light ck_count replays Light::sample, so the chunks pay off only below half that (spheres
+    // 1024^2 @ 64 spp, 16384 tiles: chunks 2902, megakernel 2973).  The wavefront runs on request,
+    // or from SP_WAVE_MIN_TILES tiles (test hook).
     int64_t wave_min = INT64_MAX, chunk_max = 24000;
     if (const char* v = std::getenv("SP_WAVE_MIN_TILES")) wave_min = std::atoll(v);
     if (const char* v = std::getenv("SP_CHUNK_MAX_TILES")) chunk_max = std::atoll(v);
-    // sample-chunk buffers: per-sample hit records and radiance, the generator store (a
-    // DirectLighting sample draws at most 34 words per light: Light::sample 2 + glossy rho 32; +2
-    // generations for the first twist and the one rng_prepare may twist ahead), chunk starts
-    const uint32_t spp_u   = p->samples_per_pixel;
-    int64_t ck_chunks = 1; // chunks per pixel, then of ck_len samples each (the last may be short)
-    while (ck_chunks < 32 && n_tiles * ck_chunks < 120000) ck_chunks *= 2;
-    if (const char* v = std::getenv("SP_CHUNKS")) ck_chunks = std::max<int64_t>(1, std::atoll(v));
-    ck_chunks              = std::min<int64_t>(ck_chunks, spp_u);
-    const uint32_t ck_len  = (uint32_t)((spp_u + ck_chunks - 1) / ck_chunks);
-    ck_chunks              = (spp_u + ck_len - 1) / ck_len;
-    const uint64_t ck_max_draws = (uint64_t)spp_u * (uint64_t)std::max(1, s->dev.n_lights) * 34;
-    const uint32_t ck_gens      = (uint32_t)((ck_max_draws + spm::MT_N - 1) / spm::MT_N + 2);
-    const double   ck_base_bytes = (double)n_tiles * 64 * spp_u * (16 + 12 + 2) +
-                                 (double)n_tiles * ck_gens * spm::MT_N * 64 * 8 + (double)ck_chunks * n_tiles * 64 * 4;
-    double ck_max_gb = 96.0;
-    if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) ck_max_gb = std::atof(v);
-    // with an image light ck_count replays Light::sample (draw counts depend on the drawn texel):
-    // the chunks then pay off only on smaller shards (spheres 1024^2 @ 64 spp, 16384 tiles: chunks
-    // 2902, megakernel 2973 Mrays/s)
+    const uint32_t spp_u = p->samples_per_pixel;
+    int64_t chunks_req = p->chunks_per_pixel;
+    if (chunks_req == 0)
+        if (const char* v = std::getenv("SP_CHUNKS")) chunks_req = std::max<int64_t>(1, std::atoll(v)); // test hook
+    const ChunkPlan cp = chunk_plan(s, n_tiles, spp_u, chunks_req);
+    double ck_max_gb = p->chunk_max_gb > 0.0f ? (double)p->chunk_max_gb : 96.0;
+    if (p->chunk_max_gb == 0.0f)
+        if (const char* v = std::getenv("SP_CHUNK_MAX_GB")) ck_max_gb = std::atof(v); // test hook
+    // budget: the caller's cap, and never more than the device can still give (the buffer held
+    // from an earlier call is freed first)
+    size_t free_b = 0, total_b = 0;
+    SP_HIP(hipMemGetInfo(&free_b, &total_b));
+    const double ck_budget = std::min(ck_max_gb * 1e9, (double)free_b + (double)s->ck_cap);
     bool image_light = false;
     for (const auto& l : s->host->lights) image_light = image_light || l.kind == SP_LIGHT_IMAGE_ENVIRONMENT;
     if (pipeline == SP_PIPELINE_AUTO) {
         if (wave_ok && n_tiles >= wave_min) pipeline = SP_PIPELINE_WAVEFRONT;
         else if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && n_tiles < (image_light ? chunk_max / 2 : chunk_max) &&
-                 ck_base_bytes <= ck_max_gb * 1e9)
+                 (double)cp.total <= ck_budget)
             pipeline = SP_PIPELINE_SAMPLE_CHUNKS;
         else pipeline = SP_PIPELINE_MEGAKERNEL; // also when the chunk buffers would not fit the budget
     }
+    if (pipeline == SP_PIPELINE_SAMPLE_CHUNKS && cp.total > s->ck_cap) {
+        if ((double)cp.total > ck_budget)
+            return fail(SP_ERR_UNSUPPORTED, "sample-chunk pipeline: buffers exceed the budget (chunk_max_gb / free "
+                                            "device memory; render fewer tiles per call)");
+        if (s->ck_buf) (void)hipFree(s->ck_buf);
+        s->ck_buf = nullptr;
+        s->ck_cap = 0;
+        const hipError_t e = hipMalloc(&s->ck_buf, cp.total);
+        if (e != hipSuccess) {
+            s->ck_buf = nullptr;
+            (void)hipGetLastError();
+            if (asked != SP_PIPELINE_AUTO) return fail(SP_ERR_HIP, std::string("sample-chunk buffers: ") + hipGetErrorString(e));
+            pipeline = SP_PIPELINE_MEGAKERNEL; // AUTO: the megakernel needs no per-sample buffers
+        } else {
+            s->ck_cap = cp.total;
+        }
+    }
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
-    int                launches = 0, parts_used = 1;
-    unsigned long long ck_camera_rays = 0, ck_samples = 0; // sample-chunk pipeline: counted on the host
-    if (pipeline == SP_PIPELINE_WAVEFRONT && wpath_ok) {
-        const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
-        if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
-        // tile slots in flight: enough waves to fill the chip several times over; each slot
-        // holds 64 pixel states (~27 KB with its mt19937_64 state), refilled from the tile list
-        int64_t slots = 32768;
-        if (const char* v = std::getenv("SP_PATH_SLOTS")) slots = std::max<int64_t>(1, std::atoll(v));
-        slots = std::min<int64_t>(slots, n_tiles);
-        const size_t need = spd::wpath_bytes_per_slot() * (size_t)slots + 16 * 256;
-        if (need > s->wp_cap) {
-            if (s->wp_buf) (void)hipFree(s->wp_buf);
-            s->wp_buf = nullptr;
-            s->wp_cap = 0;
-            SP_HIP(hipMalloc(&s->wp_buf, need));
-            s->wp_cap = need;
-        }
-        if (!s->wp_ctl) {
-            SP_HIP(hipMalloc(&s->wp_ctl, 2 * sizeof(int32_t)));
-            SP_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->wp_host), 2 * sizeof(int32_t), hipHostMallocDefault));
-            SP_HIP(hipEventCreateWithFlags(&s->wp_ev[0], hipEventDisableTiming));
-            SP_HIP(hipEventCreateWithFlags(&s->wp_ev[1], hipEventDisableTiming));
-        }
-        spd::WPathRun r{};
-        r.slots       = (int32_t)slots;
-        r.tile_ids    = p->tile_ids ? s->d_tiles : nullptr;
-        r.num_tiles   = n_tiles;
-        r.tiles_x     = (s->dev.width + 7) / 8;
-        r.spp         = p->samples_per_pixel;
-        r.integrator  = integ;
-        r.out         = d_out;
-        r.buf         = s->wp_buf;
-        r.ctl         = s->wp_ctl;
-        r.host_active = s->wp_host;
-        r.poll_ev[0]  = s->wp_ev[0];
-        r.poll_ev[1]  = s->wp_ev[1];
-        r.counters    = s->counters;
-        int iters = 0;
-        SP_HIP(hipEventRecord(s->ev0, stream));
-        SP_HIP(spd::wpath_render(s->dev, r, stream, &iters));
-        launches = 1 + 2 * iters + 1;
-    } else if (pipeline == SP_PIPELINE_WAVEFRONT) {
+    int launches = 0, parts_used = 1;
+    if (pipeline == SP_PIPELINE_WAVEFRONT) {
         const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
         if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         // Pixels in flight per pass: all requested tiles unless the state would exceed the budget
@@ -1025,9 +1062,9 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         }
         w.diag = d_diag;
         const int per_cu = spd::wave_traverse_blocks_per_cu(s->dev);
-        int       n_parts = 2;
-        if (const char* v = std::getenv("SP_WAVE_PARTS")) n_parts = std::atoi(v);
-        n_parts = std::max(1, std::min(n_parts, spd::WF_MAX_PARTS));
+        // two halves of the tile list on two streams, their shading kernels alternating (+11 %;
+        // 3 or 4 parts measured 1988 / 1821 against 2068 Mrays/s)
+        const int n_parts = std::min(2, spd::WF_MAX_PARTS);
         if (!s->ev_fork) {
             SP_HIP(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
             for (auto& e : s->ev_shade) SP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1047,8 +1084,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         for (int64_t t0 = 0; t0 < n_tiles; t0 += chunk) {
             const int64_t nt = std::min<int64_t>(chunk, n_tiles - t0);
             w.n        = nt * 64;
-            w.tile_ids = p->tile_ids ? s->d_tiles + t0 : nullptr;
-            if (!p->tile_ids && t0 > 0) {
+            w.tile_ids = d_ids ? d_ids + t0 : nullptr;
+            if (!d_ids && t0 > 0) {
                 // identity ids beyond the first chunk: materialise them
                 std::vector<int32_t> ids((size_t)nt);
                 for (int64_t i = 0; i < nt; ++i) ids[(size_t)i] = (int32_t)(t0 + i);
@@ -1098,87 +1135,38 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         }
     } else if (pipeline == SP_PIPELINE_SAMPLE_CHUNKS) {
         // sp_chunk.hip: camera rays for all (pixel, sample) at once, a per-pixel replay of the
-        // stream positions with state snapshots at chunk starts, then every (tile, chunk) shaded
-        // in parallel, and the in-order sum.  Chunks per pixel: enough work items to keep the
-        // chip busy when the slowest pixel's chain would otherwise set the frame time (~120K
-        // (tile, chunk) items was best on bunny's 2/4/8-way shards: tools/gpu_sweep_chunks.sh).
+        // stream positions into the generator store, then every (tile, chunk) shaded in parallel,
+        // and the in-order sum (buffers: chunk_plan above)
         const int    rs_words  = spd::rsqrt_words(s->dev);
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
         if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
-        const uint32_t spp       = spp_u;
-        const int64_t  chunks    = ck_chunks;
-        const uint32_t chunk_len = ck_len;
-        const size_t   n_px      = (size_t)n_tiles * 64;
-        const size_t   b_hits    = n_px * spp * 16;
-        const size_t   b_L       = n_px * spp * 12;
-        const uint32_t gens      = ck_gens; // generator store: every generation a pixel's stream reaches
-        const size_t   b_snap    = (size_t)n_tiles * gens * spm::MT_N * 64 * 8;
-        const size_t b_ctl    = (size_t)chunks * n_px * 4;
-        // per-sample draw counts from the camera pass unless an image light makes them depend on
-        // the drawn numbers (then ck_count replays Light::sample)
-        bool known_draws = s->dev.n_lights <= 1000;
-        for (const auto& l : s->host->lights)
-            if (l.kind == SP_LIGHT_IMAGE_ENVIRONMENT) known_draws = false;
-        if (const char* v = std::getenv("SP_CHUNK_REPLAY")) known_draws = known_draws && std::atoi(v) == 0;
-        const size_t b_draws  = known_draws ? n_px * spp * 2 : 0;
-        // SP_CHUNK_SPLIT=1: shading split into ck_eval + ck_occl (one shadow ray per sample and
-        // light kept in HBM).  Opt-in: exact, but slower than the fused ck_shade at every shard
-        // size measured (8-way 1374-1366 vs 1498 Mrays/s)
-        size_t b_sray = n_px * spp * (size_t)std::max(1, s->dev.n_lights) * 48;
-        bool   split  = false;
-        if (const char* v = std::getenv("SP_CHUNK_SPLIT")) split = std::atoi(v) != 0 && s->dev.n_lights <= 8;
-        const double max_gb = ck_max_gb;
-        if ((double)(b_hits + b_L + b_snap + b_ctl + b_draws + b_sray) > max_gb * 1e9) split = false;
-        if (!split) b_sray = 0;
-        const size_t need_b   = b_hits + b_L + b_snap + b_ctl + b_draws + b_sray + 4 * 256;
-        if ((double)need_b > max_gb * 1e9)
-            return fail(SP_ERR_UNSUPPORTED, "sample-chunk pipeline: buffers exceed SP_CHUNK_MAX_GB (render fewer tiles per call)");
-        if (need_b > s->ck_cap) {
-            if (s->ck_buf) (void)hipFree(s->ck_buf);
-            s->ck_buf = nullptr;
-            s->ck_cap = 0;
-            SP_HIP(hipMalloc(&s->ck_buf, need_b));
-            s->ck_cap = need_b;
-        }
+        const size_t n_px   = (size_t)n_tiles * 64;
         if (!s->ck_ctr) SP_HIP(hipMalloc(&s->ck_ctr, 2 * sizeof(int32_t)));
-        int eval_waves = 4; // ck_eval occupancy (SP_EVAL_WAVES: 2, 3 or 4 waves per SIMD)
-        if (const char* v = std::getenv("SP_EVAL_WAVES")) eval_waves = std::atoi(v);
-        const int per_cu = split ? spd::chunk_eval_blocks_per_cu(eval_waves, (size_t)rs_words * 4) : spd::chunk_blocks_per_cu(lds_bytes);
-        const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * per_cu, (n_tiles * chunks + 3) / 4));
+        const int per_cu = spd::chunk_blocks_per_cu(lds_bytes);
+        const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * per_cu, (n_tiles * cp.chunks + 3) / 4));
         char*          base = static_cast<char*>(s->ck_buf);
         spd::ChunkArgs a{};
-        a.tile_ids  = p->tile_ids ? s->d_tiles : nullptr;
-        a.num_tiles = n_tiles;
-        a.tiles_x   = (s->dev.width + 7) / 8;
-        a.spp       = spp;
-        a.chunks    = (uint32_t)chunks;
-        a.chunk_len = chunk_len;
-        a.n_px      = n_px;
-        a.hits      = reinterpret_cast<float4*>(base);
-        a.L         = reinterpret_cast<float*>(base + b_hits);
-        a.gens        = reinterpret_cast<uint64_t*>(base + b_hits + b_L);
-        a.gens_per_px = gens;
-        a.snap_ctl  = reinterpret_cast<uint32_t*>(base + b_hits + b_L + b_snap);
-        a.draws     = known_draws ? reinterpret_cast<uint16_t*>(base + b_hits + b_L + b_snap + b_ctl) : nullptr;
-        a.sray      = split ? reinterpret_cast<float4*>(base + b_hits + b_L + b_snap + b_ctl + b_draws) : nullptr;
-        a.n_lights  = s->dev.n_lights;
-        a.counter   = s->ck_ctr;
-        a.counters  = s->counters;
-        a.out       = d_out;
+        a.tile_ids    = d_ids;
+        a.num_tiles   = n_tiles;
+        a.tiles_x     = (s->dev.width + 7) / 8;
+        a.spp         = spp_u;
+        a.chunks      = (uint32_t)cp.chunks;
+        a.chunk_len   = cp.len;
+        a.n_px        = n_px;
+        a.hits        = reinterpret_cast<float4*>(base);
+        a.L           = reinterpret_cast<float*>(base + cp.b_hits);
+        a.gens        = reinterpret_cast<uint64_t*>(base + cp.b_hits + cp.b_L);
+        a.gens_per_px = cp.gens;
+        a.snap_ctl    = reinterpret_cast<uint32_t*>(base + cp.b_hits + cp.b_L + cp.b_snap);
+        a.draws       = cp.known_draws ? reinterpret_cast<uint16_t*>(base + cp.b_hits + cp.b_L + cp.b_snap + cp.b_ctl) : nullptr;
+        a.n_lights    = s->dev.n_lights;
+        a.counter     = s->ck_ctr;
+        a.counters    = s->counters;
+        a.out         = d_out;
         SP_HIP(hipMemsetAsync(s->ck_ctr, 0, 2 * sizeof(int32_t), stream));
         SP_HIP(hipEventRecord(s->ev0, stream));
-        SP_HIP(spd::chunk_render(s->dev, a, blocks, eval_waves, stream));
-        launches = split ? 5 : 4;
-        // camera rays and samples: one per inside pixel and sample (counted here, not on device)
-        int64_t inside = 0;
-        const int32_t tw = (s->dev.width + 7) / 8;
-        for (int64_t sl = 0; sl < n_tiles; ++sl) {
-            const int64_t t  = p->tile_ids ? p->tile_ids[sl] : sl;
-            const int64_t x0 = (t % tw) * 8, y0 = (t / tw) * 8;
-            inside += std::min<int64_t>(8, s->dev.width - x0) * std::min<int64_t>(8, s->dev.height - y0);
-        }
-        ck_camera_rays = s->dev.max_depth > 0 ? (unsigned long long)inside * spp : 0ull;
-        ck_samples     = (unsigned long long)inside * spp;
+        SP_HIP(spd::chunk_render(s->dev, a, blocks, stream));
+        launches = 4;
     } else {
         const int    rs_words  = spd::rsqrt_words(s->dev);
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
@@ -1191,7 +1179,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         const int lds_waves = (int)std::min<size_t>(8, (160 * 1024) / lds_bytes);
         int       variant   = integ == SP_INTEGRATOR_ITERATIVE_RRNEE ? 3 : 4;
         variant             = std::max(2, std::min(variant, lds_waves));
-        if (const char* v = std::getenv("SP_KERNEL_VARIANT")) variant = std::atoi(v);
+        if (waves_req) variant = waves_req;
         const int     per_cu  = spd::render_blocks_per_cu(integ, variant, lds_bytes);
         const int64_t max_blk = (int64_t)s->n_cu * per_cu;
         const int64_t need    = (n_tiles + 3) / 4;
@@ -1206,7 +1194,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
         spd::RenderArgs a{};
         a.out          = d_out;
-        a.tile_ids     = p->tile_ids ? s->d_tiles : nullptr;
+        a.tile_ids     = d_ids;
         a.num_tiles    = n_tiles;
         a.tiles_x      = (s->dev.width + 7) / 8;
         a.spp          = p->samples_per_pixel;
@@ -1230,33 +1218,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             a.deep        = static_cast<float*>(s->deep_buf);
             a.deep_stride = lanes;
         }
-        // SP_TILE_ORDER=1: longest-first tile order (a probe of one centre ray per pixel ranks the
-        // tiles; probe and sort are inside the timed render).  Opt-in: measured slower than the
-        // scheduler's own order on bunny at 2-8 GPUs' shards -- the frame's end is
-        // set by the slowest single tile, which no order shortens.
-        a.order = nullptr;
         SP_HIP(hipEventRecord(s->ev0, stream));
-        bool order_on = false;
-        if (const char* v = std::getenv("SP_TILE_ORDER")) order_on = std::atoi(v) != 0 && n_tiles > 1;
-        if (order_on) {
-            if ((size_t)n_tiles > s->order_cap) {
-                if (s->d_cost) (void)hipFree(s->d_cost);
-                if (s->d_order) (void)hipFree(s->d_order);
-                s->d_cost = nullptr; s->d_order = nullptr; s->order_cap = 0;
-                SP_HIP(hipMalloc(&s->d_cost, (size_t)n_tiles * sizeof(float)));
-                SP_HIP(hipMalloc(&s->d_order, (size_t)n_tiles * sizeof(int32_t)));
-                s->order_cap = (size_t)n_tiles;
-            }
-            SP_HIP(spd::launch_tile_cost(s->dev, a.tile_ids, n_tiles, a.tiles_x, s->d_cost, stream));
-            std::vector<float> cost((size_t)n_tiles);
-            SP_HIP(hipMemcpyAsync(cost.data(), s->d_cost, cost.size() * sizeof(float), hipMemcpyDeviceToHost, stream));
-            SP_HIP(hipStreamSynchronize(stream));
-            std::vector<int32_t> order((size_t)n_tiles);
-            for (size_t i = 0; i < order.size(); ++i) order[i] = (int32_t)i;
-            std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cost[(size_t)x] > cost[(size_t)y]; });
-            SP_HIP(hipMemcpyAsync(s->d_order, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice, stream));
-            a.order = s->d_order;
-        }
         // SP_TILE_DIAG=<file>: per-tile timeline {t0, t1, wave, item} (u64, s_memrealtime 100 MHz) and,
         // in a -DSP_MEGA_PROF build, shader clocks in trace / light sample / eval / occlusion
         const char*         tdiag_path = std::getenv("SP_TILE_DIAG");
@@ -1267,8 +1229,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         }
         a.tile_diag = tdiag;
         SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
-        SP_HIP(hipStreamSynchronize(stream)); // the order vector above must outlive the async copy
-        if (tdiag) {
+        if (tdiag) { // diagnostic: waits for the render
+            SP_HIP(hipStreamSynchronize(stream));
             std::vector<unsigned long long> rec((size_t)n_tiles * 8);
             SP_HIP(hipMemcpy(rec.data(), tdiag, rec.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
             (void)hipFree(tdiag);
@@ -1277,18 +1239,34 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                 std::fclose(f);
             }
         }
-        launches = order_on ? 2 : 1;
+        launches = 1;
     }
     SP_HIP(hipEventRecord(s->ev1, stream));
-    SP_HIP(hipEventSynchronize(s->ev1));
+    // stream order: without stats nothing waits -- the render is only enqueued
     if (stats) {
+        SP_HIP(hipEventSynchronize(s->ev1));
         unsigned long long c[8];
         SP_HIP(hipMemcpy(c, s->counters, sizeof(c), hipMemcpyDeviceToHost));
         float ms = 0.0f;
         SP_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
         if (pipeline == SP_PIPELINE_SAMPLE_CHUNKS) {
-            c[0] = ck_camera_rays + c[1];
-            c[2] = ck_samples;
+            // camera rays and samples: one per inside pixel and sample (counted here, not on device)
+            std::vector<int32_t> ids;
+            if (listed) {
+                ids.resize((size_t)n_tiles);
+                if (p->tile_ids) std::memcpy(ids.data(), p->tile_ids, ids.size() * sizeof(int32_t));
+                else SP_HIP(hipMemcpy(ids.data(), p->d_tile_ids, ids.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+            }
+            int64_t       inside = 0;
+            const int32_t tw     = (s->dev.width + 7) / 8;
+            for (int64_t sl = 0; sl < n_tiles; ++sl) {
+                const int64_t t = listed ? ids[(size_t)sl] : sl;
+                if (t < 0 || t >= total) continue;
+                const int64_t x0 = (t % tw) * 8, y0 = (t / tw) * 8;
+                inside += std::min<int64_t>(8, s->dev.width - x0) * std::min<int64_t>(8, s->dev.height - y0);
+            }
+            c[0] = (s->dev.max_depth > 0 ? (unsigned long long)inside * spp_u : 0ull) + c[1];
+            c[2] = (unsigned long long)inside * spp_u;
         }
         stats->rays        = c[0];
         stats->shadow_rays = c[1];
@@ -1370,7 +1348,11 @@ int sp_scene_bvh_build_info(const sp_scene* s, int32_t bvh_mode, sp_bvh_info* ou
         const sph::Scene&    h = *s->host;
         std::vector<int32_t> prims;
         size_t               part = 0;
-        const sph::Bvh       bvh  = geometry_bvh(h, bvh_mode, prims, part);
+        sp_upload_params up{};
+        up.bvh_mode = bvh_mode;
+        UploadOpts opts;
+        if (int rc0 = resolve_upload(&up, opts)) return rc0;
+        const sph::Bvh       bvh  = geometry_bvh(h, opts, prims, part);
         *out                      = sp_bvh_info{};
         out->depth                = bvh.max_depth;
         out->nodes                = (int64_t)bvh.nodes.size();
@@ -1378,8 +1360,8 @@ int sp_scene_bvh_build_info(const sp_scene* s, int32_t bvh_mode, sp_bvh_info* ou
         std::vector<int32_t> lids;
         size_t               lpart = 0;
         out->light_depth           = light_bvh(h, lids, lpart).max_depth;
-        const bool stackless       = stackless_for(std::max(out->depth, out->light_depth));
-        if (wide_enabled(bvh_mode) && !bvh.nodes.empty() && !stackless) out->wide_depth = sph::build_wide(bvh).depth;
+        const bool stackless       = stackless_for(opts, std::max(out->depth, out->light_depth));
+        if (wide_enabled(opts) && !bvh.nodes.empty() && !stackless) out->wide_depth = sph::build_wide(bvh).depth;
         out->stack_depth = stackless ? 0 : std::max(out->depth, std::max(out->wide_depth, out->light_depth)) + 1;
         return SP_OK;
     } catch (const std::exception& e) {

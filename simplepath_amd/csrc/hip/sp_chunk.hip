@@ -268,122 +268,6 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) ck_shade(Scene sc,
     wave_add(a.counters + 3, draws_total);
 }
 
-// ------------------------------------------------------- split shading: eval, then occlusion
-// ck_eval is ck_shade without the shadow queries: occlusion draws no stream words, so the
-// samples of a chunk can be shaded first (stream order) and their shadow rays traced afterwards,
-// all (pixel, sample) at once, by ck_occl.  The contribution term is formed here with
-// direct_nee's expression and added in light order by ck_occl when unoccluded -- the same
-// floating-point sequence (as the wavefront's wf_shade / wf_shadow split).
-template <int MINW>
-__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) ck_eval(Scene sc, ChunkArgs a)
-{
-    extern __shared__ uint32_t lds[];
-    const Lds      l    = lds_setup(sc, lds, false);
-    const uint32_t lane = threadIdx.x & 63u;
-    Rng            rng;
-    uint64_t       shadow_total = 0, draws_total = 0;
-    while (true) {
-        const int64_t item = grab(a.counter + 1);
-        if (item >= a.num_tiles * (int64_t)a.chunks) break;
-        const int64_t  slot = item / a.chunks;
-        const uint32_t c    = (uint32_t)(item % a.chunks);
-        const Px       px   = pixel(sc, a, slot, lane);
-        const size_t   p    = (size_t)slot * 64 + lane;
-        const uint32_t i0   = c * a.chunk_len;
-        const uint32_t i1   = min(a.spp, i0 + a.chunk_len);
-        if (px.inside && i0 < i1) {
-            const uint32_t st = a.snap_ctl[(size_t)c * a.n_px + p];
-            rng.base  = a.gens + (size_t)slot * a.gens_per_px * (MT_N * 64) + lane;
-            rng.idx   = (int)(st & 0xffffu);
-            rng.cur   = (int)(st >> 16);
-            rng.lin   = 1;
-            rng.pre   = 1;
-            rng.ready = 1;
-            rng.draws = 0;
-            rng.pfn   = 0;
-            for (uint32_t i = i0; i < i1; ++i) {
-                rng_prepare(rng);
-                const float4   rec  = a.hits[(size_t)i * a.n_px + p];
-                const uint32_t code = __float_as_uint(rec.y);
-                if (code == NO_HIT) continue;
-                const Ray   ray = camera_ray_px(sc, px, i, l.q);
-                const Hit   h{ rec.x, code, rec.z, rec.w };
-                const Isect is  = finish_hit(sc, h, ray, l.q);
-                const f3    wo  = neg(ray.d);
-                for (int li = 0; li < sc.n_lights; ++li) { // direct_nee, up to the occlusion test
-                    const Light   lt = uload_light(sc.lights + li);
-                    const LSample ls = light_sample(sc, lt, is.p, is.n, next2D(rng), l.q);
-                    float4        r0 = make_float4(0, 0, 0, 0), r1 = r0, r2 = r0;
-                    if (!(ls.pdf == 0.0f || cblack(ls.L))) {
-                        const f3  wi = ls.ray.d;
-                        const rgb f  = material_eval(sc, is.material, wo, wi, is.n, rng, l.q);
-                        if (!cblack(f)) {
-                            const rgb t = cdivs(cscale(cmul(f, ls.L), abs_f(dot(wi, is.n))), ls.pdf);
-                            r0 = make_float4(ls.ray.o.x, ls.ray.o.y, ls.ray.o.z, ls.tmin);
-                            r1 = make_float4(wi.x, wi.y, wi.z, ls.tmax);
-                            r2 = make_float4(t.r, t.g, t.b, 1.0f);
-                            ++shadow_total;
-                        }
-                    }
-                    float4* q = a.sray + (((size_t)i * a.n_lights + li) * 3) * a.n_px + p;
-                    q[0]          = r0;
-                    q[a.n_px]     = r1;
-                    q[2 * a.n_px] = r2;
-                }
-            }
-            draws_total += rng.draws;
-        }
-    }
-    wave_add(a.counters + 1, shadow_total);
-    wave_add(a.counters + 3, draws_total);
-}
-
-__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_occl(Scene sc, ChunkArgs a)
-{
-    extern __shared__ uint32_t lds[];
-    const Lds      l    = lds_setup(sc, lds, true);
-    const uint32_t lane = threadIdx.x & 63u;
-    const int64_t  item = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    if (item >= a.num_tiles * (int64_t)a.spp) return;
-    const int64_t  slot = item % a.num_tiles;
-    const uint32_t i    = (uint32_t)(item / a.num_tiles);
-    const Px       px   = pixel(sc, a, slot, lane);
-    const size_t   p    = (size_t)slot * 64 + lane;
-    if (px.inside && __float_as_uint(a.hits[(size_t)i * a.n_px + p].y) != NO_HIT) {
-        rgb L = mkc(0, 0, 0);
-        for (int li = 0; li < a.n_lights; ++li) { // light order, as direct_nee
-            const float4* q  = a.sray + (((size_t)i * a.n_lights + li) * 3) * a.n_px + p;
-            const float4  r2 = q[2 * a.n_px];
-            if (r2.w == 0.0f) continue;
-            const float4 r0 = q[0], r1 = q[a.n_px];
-            Ray          ray;
-            ray.o = mk(r0.x, r0.y, r0.z);
-            ray.d = mk(r1.x, r1.y, r1.z);
-            if (!scene_any(sc, ray, r0.w, r1.w, l.st)) L = cadd(L, mkc(r2.x, r2.y, r2.z));
-        }
-        a.L[((size_t)i * 3 + 0) * a.n_px + p] = L.r;
-        a.L[((size_t)i * 3 + 1) * a.n_px + p] = L.g;
-        a.L[((size_t)i * 3 + 2) * a.n_px + p] = L.b;
-    }
-}
-
-using ChunkFn = void (*)(Scene, ChunkArgs);
-static ChunkFn eval_kernel(int waves)
-{
-    switch (waves) {
-    case 2: return ck_eval<2>;
-    case 3: return ck_eval<3>;
-    default: return ck_eval<4>;
-    }
-}
-int chunk_eval_blocks_per_cu(int eval_waves, size_t lds_bytes)
-{
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, eval_kernel(eval_waves), 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess)
-        return 1;
-    return n > 0 ? n : 1;
-}
-
 // ------------------------------------------------------------------------------ resolve
 __global__ void __launch_bounds__(256) ck_sum(Scene sc, ChunkArgs a)
 {
@@ -402,21 +286,11 @@ __global__ void __launch_bounds__(256) ck_sum(Scene sc, ChunkArgs a)
     a.out[(size_t)p * 3 + 2] = acc.b;
 }
 
-// ck_shade occupancy request (SP_CK_WAVES, waves per SIMD): default 4 (128 VGPRs, ~210 B spill);
-// 2 = the compiler's choice (192 VGPRs, no spill), 3 = 168 VGPRs.  Bunny 8-way shard per GPU:
+// ck_shade occupancy: 4 waves per SIMD (128 VGPRs, ~116 B spill).  Bunny 8-way shard per GPU:
 // 1686 / 2039 / 2161 Mrays/s at 2 / 3 / 4 waves (profiles/r02/s5): the chunk kernel's lanes wait
 // on generator-store loads, and more waves hide them better than fewer spills do.
 typedef void (*CkShadeFn)(Scene, ChunkArgs);
-static CkShadeFn shade_kernel()
-{
-    const char* v = std::getenv("SP_CK_WAVES");
-    switch (v ? std::atoi(v) : 4) {
-    case 2: return ck_shade<1>;
-    case 3: return ck_shade<3>;
-    case 5: return ck_shade<5>;
-    default: return ck_shade<4>;
-    }
-}
+static CkShadeFn shade_kernel() { return ck_shade<4>; }
 
 int chunk_blocks_per_cu(size_t lds_bytes)
 {
@@ -425,7 +299,7 @@ int chunk_blocks_per_cu(size_t lds_bytes)
     return n > 0 ? n : 1;
 }
 
-hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int eval_waves, hipStream_t stream)
+hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, hipStream_t stream)
 {
     const size_t rs_bytes    = (size_t)rsqrt_words(sc) * 4;
     const size_t stack_bytes = (size_t)WAVES_PER_BLOCK * sc.stack_words * 64 * 4;
@@ -437,16 +311,8 @@ hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_bloc
     hipLaunchKernelGGL(ck_count, dim3((unsigned)((a.num_tiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
                        dim3(64 * WAVES_PER_BLOCK), rs_bytes, stream, sc, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (a.sray) {
-        hipLaunchKernelGGL(eval_kernel(eval_waves), dim3((unsigned)persistent_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes,
-                           stream, sc, a);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL(ck_occl, dim3((unsigned)((cam_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
-                           dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes, stream, sc, a);
-    } else {
-        hipLaunchKernelGGL(shade_kernel(), dim3((unsigned)persistent_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes,
-                           stream, sc, a);
-    }
+    hipLaunchKernelGGL(shade_kernel(), dim3((unsigned)persistent_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes,
+                       stream, sc, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(ck_sum, dim3((unsigned)((a.n_px + 255) / 256)), dim3(256), 0, stream, sc, a);
     return hipGetLastError();

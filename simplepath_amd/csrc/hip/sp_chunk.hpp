@@ -20,8 +20,6 @@ struct ChunkArgs {
                                    // mt19937_64 stream, written once by ck_count, read by ck_shade
     uint32_t            gens_per_px;
     uint32_t*           snap_ctl;  // [chunks][n_px] stream position at each chunk start: idx | gen << 16
-    float4*             sray;      // split shading: [spp][n_lights][3][n_px] shadow ray {o, tmin},
-                                   // {d, tmax}, {contribution, flag}; nullptr: fused ck_shade
     int32_t             n_lights;
     int32_t*            counter;   // [2] work queues of ck_count and ck_shade (zeroed by the caller)
     unsigned long long* counters;  // stats: [1] shadow rays, [3] RNG draws
@@ -29,7 +27,6 @@ struct ChunkArgs {
 };
 
 int        chunk_blocks_per_cu(size_t lds_bytes);
-hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int eval_waves, hipStream_t stream);
-int        chunk_eval_blocks_per_cu(int eval_waves, size_t lds_bytes);
+hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, hipStream_t stream);
 
 } // namespace spd

@@ -137,7 +137,6 @@ struct RenderArgs {
     unsigned long long* counters; // [rays, shadow_rays, samples, draws]
     float*          deep;       // recursive integrators, max_depth > 32: per-lane level records
     size_t          deep_stride;// lanes of the launch (= blocks * 256)
-    const int32_t*  order;      // processing order of the tile slots (nullptr: slot order)
     unsigned long long* tile_diag; // SP_TILE_DIAG: per slot {t0, t1 (s_memrealtime), wave, item, 4 stage clocks}
 };
 

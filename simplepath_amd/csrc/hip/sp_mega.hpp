@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
         const int64_t item = __shfl(grabbed, 0, 64);
         if (item >= args.num_tiles) break;
-        const int64_t slot = args.order ? args.order[item] : item; // longest-first order, if given
+        const int64_t  slot    = item;
         const uint64_t t_start = args.tile_diag ? __builtin_amdgcn_s_memrealtime() : 0;
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
         const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
@@ -128,157 +128,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Per-lane sample regeneration for the iterative integrators.  sp_render_kernel runs the
-// samples of its 64 pixels in lock step: every sample costs the wave its LONGEST path.  Here the
-// bounce loop body of BruteForceIntegratorIterative(RR) / IntegratorIterativeRRNEE
-// (Integrator.cpp:160, :211, :550) is one step; a lane whose path ends adds its L to the pixel's
-// sum and starts its next sample at the next step, so all lanes keep executing the same step
-// code (trace, material sample, NEE, roulette) on whatever sample they are at.  Per pixel the
-// sample order, RNG draw order and arithmetic are unchanged (bit-identical images).
-struct PathState {
-    Ray   ray;
-    float tmin;
-    rgb   L, thr;
-    int   depth;
-};
-
-// One iteration of the reference's `for (depth = 0; depth < max_depth; ++depth)` body; returns
-// true when the path has ended (L final).
-template <int INTEG>
-__device__ __forceinline__ bool path_step(Ctx& c, PathState& ps)
-{
-    constexpr bool  NEE    = INTEG == SP_INTEGRATOR_ITERATIVE_RRNEE;
-    constexpr bool  RR     = INTEG != SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE;
-    constexpr float rr_cut = 0.1f;
-    const Query     qr     = trace(c, ps.ray, ps.tmin, k_infinite);
-    if (qr.geom) {
-        const f3      wo = neg(ps.ray.d);
-        const f3      n  = qr.is.n;
-        const MSample s  = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
-        if (s.pdf == 0.0f || cblack(s.color)) return true;
-        if constexpr (NEE) {
-            for (int li = 0; li < c.sc.n_lights; ++li)
-                ps.L = cadd(ps.L, cmul(ps.thr, estimate_direct_mis(c, c.sc.lights[li], qr.is.p, n, wo, qr.is.material)));
-        }
-        const f3    next_o = ray_at(ps.ray, qr.is.t);
-        const f3    wi     = s.dir;
-        const float cosine = abs_f(dot(wi, n));
-        ps.thr             = cmul(ps.thr, cdivs(cscale(s.color, cosine), s.pdf));
-        if (RR && ps.depth >= c.sc.rr_depth) {
-            const float lum = luminance(ps.thr);
-            if (lum < rr_cut) {
-                const float qv = std_max(0.05f, lum / rr_cut);
-                if (next1D(c.rng) < qv) ps.thr = cdivs(ps.thr, qv);
-                else return true;
-            }
-        }
-        ps.ray.o = next_o;
-        ps.ray.d = wi;
-        ps.tmin  = ray_offset(cosine);
-        ++ps.depth;
-        return ps.depth >= c.sc.max_depth;
-    }
-    if (qr.lh.hit) ps.L = cadd(ps.L, cmul(ps.thr, light_hit_L(c.sc, qr.lh, ps.ray.d, c.q)));
-    return true;
-}
-
-template <int INTEG, int MINW>
-__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_regen(Scene sc, RenderArgs args)
-{
-    extern __shared__ uint32_t lds[];
-    const int tid  = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int rs_words = rsqrt_words(sc);
-    for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
-    libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
-    __syncthreads();
-    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
-    Stack st{ lds + rs_words + wave * sc.stack_words * 64, lane, sc.stack_depth };
-
-    const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;
-    Rng          rng;
-    rng.base = args.mt_state + gwave * (2 * MT_N * 64) + lane;
-
-    uint32_t rays_total = 0, shadow_total = 0, samples_total = 0, draws_total = 0;
-    const uint32_t dx = morton_decode_1((uint32_t)lane);
-    const uint32_t dy = morton_decode_1((uint32_t)lane >> 1);
-    while (true) {
-        int grabbed = 0;
-        if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
-        const int64_t item = __shfl(grabbed, 0, 64);
-        if (item >= args.num_tiles) break;
-        const int64_t slot = args.order ? args.order[item] : item; // longest-first order, if given
-        const uint64_t t_start = args.tile_diag ? __builtin_amdgcn_s_memrealtime() : 0;
-        const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
-        const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
-        const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
-        const bool     inside = (int)px < sc.width && (int)py < sc.height;
-        rgb            acc    = mkc(0, 0, 0);
-        const uint32_t pix_seed = (px << 16u) | py;
-        const uint32_t seed2d   = pix_seed ^ 0x6184faf4u; // RSequenceSampler m_seed_2D (main.cpp:67)
-        if (inside) rng_seed(rng, pix_seed ^ 0xb0ae9d99u);  // get_integrator_sampler (main.cpp:73)
-        Ctx       c{ sc, rng, q, st, 0u, 0u };
-        uint32_t  i      = 0;
-        bool      active = inside && args.spp > 0;
-        bool      fresh  = true;
-        PathState ps;
-        while (__any(active)) {
-            if (active) {
-                if (fresh) {
-                    // RSequenceSampler::get_next_2D + PerspectiveCamera::generate_ray (main.cpp:95-97)
-                    const float sx = rseq_component(seed2d, sc.alpha2_0, i);
-                    const float sy = rseq_component(seed2d, sc.alpha2_1, i);
-                    const float fx = (float)(int)px + sx;
-                    const float fy = (float)(int)py + sy;
-                    ps.ray.o = sc.camera.p;
-                    ps.ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
-                    ps.tmin  = k_ray_epsilon;
-                    ps.L     = mkc(0, 0, 0);
-                    ps.thr   = mkc(1, 1, 1);
-                    ps.depth = 0;
-                    fresh    = false;
-                }
-                rng_prepare(rng);
-                const bool end = (sc.max_depth <= 0) || path_step<INTEG>(c, ps);
-                if (end) {
-                    acc = cadd(acc, ps.L); // image(p) += integrate(...)
-                    ++i;
-                    fresh  = true;
-                    active = i < args.spp;
-                }
-            }
-        }
-        if (inside) {
-            acc = cdivs(acc, (float)args.spp); // image(p) /= num_pixel_samples
-            rays_total += c.rays;
-            shadow_total += c.shadow;
-            samples_total += args.spp;
-            draws_total += rng.draws;
-        }
-        float* o = args.out + ((size_t)slot * 64 + lane) * 3;
-        o[0]     = acc.r;
-        o[1]     = acc.g;
-        o[2]     = acc.b;
-        if (args.tile_diag && lane < 8) {
-            const uint64_t t_end  = __builtin_amdgcn_s_memrealtime();
-            const uint64_t rec[8] = { t_start, t_end, (uint64_t)gwave, (uint64_t)item, 0, 0, 0, 0 };
-            args.tile_diag[(size_t)slot * 8 + lane] = rec[lane];
-        }
-    }
-    unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
-    for (int k = 0; k < 4; ++k) {
-        unsigned long long s = v[k];
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
-        if (lane == 0 && s) atomicAdd(args.counters + k, s);
-    }
-}
-
 using KernelFn = void (*)(Scene, RenderArgs);
 KernelFn mega_direct(int variant);
-KernelFn mega_iterative(int integ, bool regen);
-KernelFn mega_rrnee(bool regen, bool merged, int waves);
+KernelFn mega_iterative(int integ);
+KernelFn mega_rrnee(bool merged, int waves);
 KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 

@@ -44,23 +44,4 @@ hipError_t wave_render(const Scene& sc, const WaveArgs& w, float* out, int trave
                        const hipEvent_t* join, hipEvent_t* shade_done, int* parts_out);
 int        wave_traverse_blocks_per_cu(const Scene& sc);
 
-// Wavefront multi-bounce pipeline (sp_wpath.hip): BruteForceIterative(RR), IterativeRRNEE.
-struct WPathRun {
-    int32_t             slots;       // tile slots in flight (64 pixels each)
-    const int32_t*      tile_ids;    // device tile list (nullptr: identity)
-    int64_t             num_tiles;
-    int32_t             tiles_x;
-    uint32_t            spp;
-    int32_t             integrator;
-    float*              out;         // tile-packed output
-    void*               buf;         // wpath_bytes_per_slot() * slots bytes (+ alignment slack)
-    int32_t*            ctl;         // device int32[2]: next tile, active slots
-    int32_t*            host_active; // pinned host int32[2]
-    hipEvent_t          poll_ev[2];
-    unsigned long long* counters;    // [rays, shadow, samples, draws]
-};
-bool       wpath_supports(int integrator);
-size_t     wpath_bytes_per_slot();
-hipError_t wpath_render(const Scene& sc, const WPathRun& r, hipStream_t stream, int* iterations);
-
 } // namespace spd

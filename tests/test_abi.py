@@ -50,3 +50,27 @@ def test_render_requires_upload(scene_dir):
         raise AssertionError("expected SP_ERR_STATE")
     except sp.SimplePathError as e:
         assert e.code == _abi.SP_ERR_STATE
+
+
+def test_abi_version_and_struct_layout():
+    # ABI 4: sp_render_params grew the device tile list, occupancy and chunk fields; the ctypes
+    # mirror must match the header's layout
+    import ctypes as C
+    text = open(HEADER).read()
+    assert re.search(r"#define SP_ABI_VERSION 4\b", text)
+    assert C.sizeof(_abi.sp_render_params) == 72  # gcc on include/simplepath_hip.h: 72, 40, 60, 32
+    assert _abi.sp_render_params.d_tile_ids.offset == 40 and _abi.sp_render_params.reserved.offset == 60
+    assert C.sizeof(_abi.sp_upload_params) == 32
+
+
+def test_upload_params_validated_before_the_device(scene_dir):
+    # argument errors come back as SP_ERR_ARG before any device is touched (this container has none)
+    import ctypes as C
+    scene = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp"))
+    for field, value in (("walk", 7), ("bvh_mode", 2), ("sah_leaf", 9), ("stack_max_levels", -1)):
+        p = _abi.sp_upload_params()
+        setattr(p, field, value)
+        assert _abi.lib().sp_scene_upload_ex(scene.handle, 0, C.byref(p)) == _abi.SP_ERR_ARG, field
+    p = _abi.sp_upload_params()
+    p.reserved[1] = 3
+    assert _abi.lib().sp_scene_upload_ex(scene.handle, 0, C.byref(p)) == _abi.SP_ERR_ARG

@@ -1,0 +1,144 @@
+"""The C-ABI render boundary on the device (include/simplepath_hip.h, ABI 4):
+
+  * stream order -- sp_render_tiles without stats only enqueues: two renders and a dependent
+    kernel queue back to back on one stream with no host wait, and the result is bit-exact;
+  * the device tile list (d_tile_ids): nothing crosses to the host;
+  * the occupancy request (waves_per_simd) and the chunk count (chunks_per_pixel) change how the
+    image is computed, never the image;
+  * argument validation (reserved fields, unknown flags, both tile lists, occupancy ranges).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import simplepath_amd as sp
+from simplepath_amd import _abi
+
+pytestmark = pytest.mark.gpu
+
+
+def load(scene_dir, name, w, h, bvh=0):
+    s = sp.Scene.from_file(os.path.join(scene_dir, name))
+    s.set_resolution(w, h)
+    s.upload(device=0, bvh_mode=bvh)
+    return s
+
+
+def test_stream_ordered_renders_and_dependent_kernel(scene_dir):
+    s = load(scene_dir, "bunny.sp", 256, 160)
+    n = sp.TileScheduler(256, 160).get_num_tiles()
+    a_ids = np.arange(0, n, 2, dtype=np.int32)
+    b_ids = np.arange(1, n, 2, dtype=np.int32)
+    ref_a, _ = sp.render_tiles(s, "direct_lighting", 16, a_ids, pipeline="megakernel")
+    ref_b, _ = sp.render_tiles(s, "direct_lighting", 16, b_ids, pipeline="megakernel")
+    dev = torch.device("cuda:0")
+    d_a = torch.from_numpy(a_ids).to(dev)
+    d_b = torch.from_numpy(b_ids).to(dev)
+    out_a = torch.zeros((a_ids.size, 64, 3), dtype=torch.float32, device=dev)
+    out_b = torch.zeros_like(out_a)
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        for out, d in ((out_a, d_a), (out_b, d_b)):
+            r = sp.render_tiles_device(s, "direct_lighting", 16, None, out.data_ptr(), stream.cuda_stream,
+                                       pipeline="megakernel", stats=False, d_tile_ids=d.data_ptr(),
+                                       num_tiles=d.numel())
+            assert r is None
+        busy = not stream.query()  # the renders were only enqueued: the stream still has work
+        both = out_a + out_b       # a dependent kernel behind them, still without a host wait
+    stream.synchronize()
+    assert busy, "sp_render_tiles waited for the render although no stats were requested"
+    assert np.array_equal(out_a.cpu().numpy().view(np.uint32), ref_a.view(np.uint32))
+    assert np.array_equal(out_b.cpu().numpy().view(np.uint32), ref_b.view(np.uint32))
+    assert np.array_equal(both.cpu().numpy(), ref_a + ref_b)
+
+
+@pytest.mark.parametrize("pipeline", ["megakernel", "chunks", "wavefront"])
+def test_device_tile_list(scene_dir, pipeline):
+    s = load(scene_dir, "bunny.sp", 96, 64, bvh=1)
+    ids = np.random.default_rng(3).permutation(sp.TileScheduler(96, 64).get_num_tiles())[:37].astype(np.int32)
+    ref, rst = sp.render_tiles(s, "direct_lighting", 4, ids, pipeline=pipeline)
+    d = torch.from_numpy(ids).cuda()
+    out = torch.zeros((ids.size, 64, 3), dtype=torch.float32, device="cuda:0")
+    st = sp.render_tiles_device(s, "direct_lighting", 4, None, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                pipeline=pipeline, d_tile_ids=d.data_ptr(), num_tiles=ids.size)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert (st.rays, st.shadow_rays, st.samples, st.rng_draws) == (rst.rays, rst.shadow_rays, rst.samples, rst.rng_draws)
+
+
+@pytest.mark.parametrize("integrator,waves", [("direct_lighting", (1, 2, 3, 4)), ("iterative_rrnee", (2, 3, 4))])
+def test_waves_per_simd_variants_identical(scene_dir, integrator, waves):
+    s = load(scene_dir, "elf_small.sp", 40, 56)
+    ref, rst = sp.render_tiles(s, integrator, 3, pipeline="megakernel")
+    for w in waves:
+        out, st = sp.render_tiles(s, integrator, 3, pipeline="megakernel", waves_per_simd=w)
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), w
+        assert (st.rays, st.rng_draws) == (rst.rays, rst.rng_draws)
+
+
+def test_chunks_per_pixel_identical(scene_dir):
+    s = load(scene_dir, "bunny.sp", 72, 40)
+    ref, _ = sp.render_tiles(s, "direct_lighting", 9, pipeline="megakernel")
+    for c in (1, 2, 4, 9):
+        out, st = sp.render_tiles(s, "direct_lighting", 9, pipeline="chunks", chunks_per_pixel=c)
+        assert st.pipeline == sp.PIPELINES["chunks"]
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), c
+
+
+def test_chunk_budget_falls_back_under_auto(scene_dir):
+    # a budget too small for the chunk buffers: AUTO renders with the megakernel, an explicit
+    # request is refused
+    s = load(scene_dir, "bunny.sp", 72, 40)
+    out, st = sp.render_tiles(s, "direct_lighting", 4, chunk_max_gb=1e-6)
+    assert st.pipeline == sp.PIPELINES["megakernel"]
+    with pytest.raises(sp.SimplePathError):
+        sp.render_tiles(s, "direct_lighting", 4, pipeline="chunks", chunk_max_gb=1e-6)
+
+
+def test_render_params_validation(scene_dir):
+    s = load(scene_dir, "bunny.sp", 32, 32)
+    bad = [dict(waves_per_simd=5), dict(waves_per_simd=-1)]
+    for kw in bad:
+        with pytest.raises(sp.SimplePathError):
+            sp.render_tiles(s, "direct_lighting", 1, **kw)
+    with pytest.raises(sp.SimplePathError):
+        sp.render_tiles(s, "whitted", 1, waves_per_simd=3)  # one variant only
+    with pytest.raises(sp.SimplePathError):
+        sp.render_tiles(s, "iterative_rrnee", 1, waves_per_simd=1)
+    with pytest.raises(sp.SimplePathError):
+        sp.render_tiles(s, "direct_lighting", 1, chunks_per_pixel=-2)
+    import ctypes as C
+    for field, value in (("reserved", 1), ("flags", 64)):
+        p, keep = sp._params("direct_lighting", 1, None)
+        if field == "reserved":
+            p.reserved[0] = value
+        else:
+            p.flags = value
+        out = torch.zeros((16, 64, 3), dtype=torch.float32, device="cuda:0")
+        rc = _abi.lib().sp_render_tiles(s.handle, C.byref(p), C.c_void_p(out.data_ptr()), None)
+        assert rc == _abi.SP_ERR_ARG, field
+    d = torch.zeros(4, dtype=torch.int32, device="cuda:0")
+    p, keep = sp._params("direct_lighting", 1, np.arange(4))
+    p.d_tile_ids = C.c_void_p(d.data_ptr())
+    out = torch.zeros((4, 64, 3), dtype=torch.float32, device="cuda:0")
+    assert _abi.lib().sp_render_tiles(s.handle, C.byref(p), C.c_void_p(out.data_ptr()), None) == _abi.SP_ERR_ARG
+
+
+def test_upload_options_are_part_of_the_residency(scene_dir):
+    # re-uploading with other accelerator options really rebuilds (the options are part of the
+    # cache key), and every option gives the same image on the reference BVH
+    s = sp.Scene.from_file(os.path.join(scene_dir, "material_spheres_ibl.sp"))
+    s.set_resolution(24, 48)
+    s.upload(0, 1)
+    ref, rst = sp.render_tiles(s, "iterative_rrnee", 3)
+    for kw in (dict(env_replay=True), dict(stackless=True), dict(stack_max_levels=1), dict(wide_bvh=False)):
+        s.upload(0, 1, **kw)
+        out, st = sp.render_tiles(s, "iterative_rrnee", 3)
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), kw
+        if kw.get("stackless") or kw.get("stack_max_levels"):
+            assert st.stack_depth == 0
+        else:
+            assert st.stack_depth == rst.stack_depth

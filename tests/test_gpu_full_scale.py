@@ -124,16 +124,15 @@ def test_full_scale_lucy_every_pipeline(pipeline):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("guide", ["1", "0"])
 @pytest.mark.parametrize("bvh", [1, 0])
-def test_full_scale_spheres_image_light(monkeypatch, bvh, guide):
+def test_full_scale_spheres_image_light(bvh, guide):
     # configs[1] at full size: the 4096x2048 map's Distribution2D (8192-entry marginal / conditional
     # CDFs, the shifted, partly unsorted cdf the reference's normalisation leaves) sampled through
-    # the guide tables (SP_ENV_GUIDE=1, the default) and through the replayed upper_bound (0).
+    # the guide tables (the default) and through the replayed upper_bound (sp_upload_params.env_replay).
     # Bit-exact with the reference-order BVH; the SAH BVH (3 nodes over 4 spheres) within the
     # north-star tolerance.  Every pipeline AUTO may pick is covered: megakernel (the 1-GPU frame)
     # and the sample chunks (image light: ck_count replays Light::sample).
-    monkeypatch.setenv("SP_ENV_GUIDE", guide)
     g, s = full_scene("spheres")
-    s.upload(device=0, bvh_mode=bvh)
+    s.upload(device=0, bvh_mode=bvh, env_replay=guide == "0")
     ids = g["tile_ids"].astype(np.int32)
     ref = g["radiance"]
     for pipeline in ("megakernel", "chunks"):

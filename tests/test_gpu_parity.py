@@ -23,10 +23,10 @@ def rel_l2(a, b):
     return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30))
 
 
-def load(scene_dir, name, w, h, bvh):
+def load(scene_dir, name, w, h, bvh, **upload_options):
     s = sp.Scene.from_file(os.path.join(scene_dir, name))
     s.set_resolution(w, h)
-    s.upload(device=0, bvh_mode=bvh)
+    s.upload(device=0, bvh_mode=bvh, **upload_options)
     return s
 
 
@@ -104,29 +104,14 @@ def test_vs_glibc_oracle_bitexact(scene_dir, integrator):
 @pytest.mark.parametrize("integrator", ["direct_lighting", "brute_force_iterative_rr", "iterative_rrnee", "whitted",
                                         "brute_force"])
 @pytest.mark.parametrize("guide", ["1", "0"])
-def test_image_environment_light_bitexact(scene_dir, monkeypatch, integrator, guide):
+def test_image_environment_light_bitexact(scene_dir, integrator, guide):
     # ImageBasedEnvironmentLight: Distribution2D sampling (guide tables, or the replayed libstdc++
-    # upper_bound with SP_ENV_GUIDE=0), MIS pdf, escaping-ray lookups
-    monkeypatch.setenv("SP_ENV_GUIDE", guide)
-    s = load(scene_dir, "material_spheres_ibl.sp", 24, 48, bvh=1)
+    # upper_bound: sp_upload_params.env_replay), MIS pdf, escaping-ray lookups
+    s = load(scene_dir, "material_spheres_ibl.sp", 24, 48, bvh=1, env_replay=guide == "0")
     g, gst = sp.render_tiles(s, integrator, 4)
     c, cst = _oracle.render(s, sp.string_to_integrator_type(integrator), 4, variant="glibc")
     assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), (integrator, rel_l2(g, c))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("scene", ["bunny.sp", "material_spheres_ibl.sp"])
-def test_tile_order_is_invisible(scene_dir, scene, monkeypatch):
-    # longest-first tile order only changes which wave takes which tile, never a pixel's bits
-    s = load(scene_dir, scene, 72, 40, bvh=0)
-    monkeypatch.setenv("SP_TILE_ORDER", "1")
-    a, ast = sp.render_tiles(s, "direct_lighting", 3, pipeline="megakernel")
-    monkeypatch.setenv("SP_TILE_ORDER", "0")
-    b, bst = sp.render_tiles(s, "direct_lighting", 3, pipeline="megakernel")
-    assert ast.launches == 2 and bst.launches == 1
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
-    assert (ast.rays, ast.shadow_rays, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.rng_draws)
 
 
 @pytest.mark.parametrize("scene,bvh", [("bunny.sp", 0), ("material_spheres.sp", 1), ("material_spheres_ibl.sp", 0)])
@@ -150,14 +135,11 @@ def test_sample_chunks_equal_megakernel(scene_dir, monkeypatch, scene, bvh, chun
     # ray / draw counts.  Chunk counts that do not divide spp (13) leave a short last chunk; "0" =
     # automatic (16 for this many tiles).  Draw counts come from the camera pass, or from the
     # Light::sample replay (image light, or SP_CHUNK_REPLAY=1).
-    if chunks != "0":
-        monkeypatch.setenv("SP_CHUNKS", chunks)
     monkeypatch.setenv("SP_CHUNK_REPLAY", replay)
-    monkeypatch.setenv("SP_CHUNK_SPLIT", "1" if chunks in ("3", "7") else "0")  # eval + occlusion split
     s = load(scene_dir, scene, 72, 40, bvh=bvh)
     m, mst = sp.render_tiles(s, "direct_lighting", 13, pipeline="megakernel")
-    c, cst = sp.render_tiles(s, "direct_lighting", 13, pipeline="chunks")
-    assert cst.pipeline == 3 and cst.launches in (4, 5)  # 5: split eval + occlusion
+    c, cst = sp.render_tiles(s, "direct_lighting", 13, pipeline="chunks", chunks_per_pixel=int(chunks))
+    assert cst.pipeline == 3 and cst.launches == 4
     assert np.array_equal(m.view(np.uint32), c.view(np.uint32)), rel_l2(c, m)
     assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
         (cst.rays, cst.shadow_rays, cst.samples, cst.rng_draws)
@@ -173,7 +155,7 @@ def test_sample_chunks_tile_subset_matches_oracle(scene_dir):
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
 
 
-def test_wavefront_two_parts(scene_dir, monkeypatch):
+def test_wavefront_two_parts(scene_dir):
     # >= 32768 pixels in flight: two interleaved parts on two streams (ragged: odd tile count)
     s = load(scene_dir, "bunny.sp", 264, 128, bvh=0)
     m, _ = sp.render_tiles(s, "direct_lighting", 2, pipeline="megakernel")
@@ -184,26 +166,6 @@ def test_wavefront_two_parts(scene_dir, monkeypatch):
     r, rst = sp.render_tiles(s, "direct_lighting", 2, ids, pipeline="wavefront")
     assert rst.parts == 2
     assert np.array_equal(r, w[ids])
-    monkeypatch.setenv("SP_WAVE_PARTS", "1")
-    one, ost = sp.render_tiles(s, "direct_lighting", 2, pipeline="wavefront")
-    assert ost.parts == 1
-    assert np.array_equal(one, w)
-
-
-@pytest.mark.parametrize("parts", ["3", "4"])
-def test_wavefront_more_parts(scene_dir, monkeypatch, parts):
-    # 1600 tiles dealt round-robin in blocks of 240 to 3 or 4 overlapped parts (ragged last block)
-    s = load(scene_dir, "bunny.sp", 512, 200, bvh=0)
-    monkeypatch.setenv("SP_WAVE_PARTS", "1")
-    one, ost = sp.render_tiles(s, "direct_lighting", 1, pipeline="wavefront")
-    monkeypatch.setenv("SP_WAVE_PARTS", parts)
-    many, mst = sp.render_tiles(s, "direct_lighting", 1, pipeline="wavefront")
-    assert ost.parts == 1 and mst.parts == int(parts)
-    assert np.array_equal(one.view(np.uint32), many.view(np.uint32))
-    assert (ost.rays, ost.shadow_rays, ost.rng_draws) == (mst.rays, mst.shadow_rays, mst.rng_draws)
-    ids = np.random.default_rng(7).permutation(one.shape[0]).astype(np.int32)
-    sub, _ = sp.render_tiles(s, "direct_lighting", 1, ids, pipeline="wavefront")
-    assert np.array_equal(sub, one[ids])
 
 
 def test_wavefront_tile_chunks(scene_dir, monkeypatch):
@@ -232,36 +194,9 @@ def test_mandelbrot_full_frame_vs_reference(scene_dir):
 
 def test_wavefront_rejects_other_integrators(scene_dir):
     s = load(scene_dir, "bunny.sp", 16, 16, bvh=0)
-    for integ in ("whitted", "brute_force", "mandelbrot"):
+    for integ in ("whitted", "brute_force", "mandelbrot", "iterative_rrnee", "brute_force_iterative"):
         with pytest.raises(sp.SimplePathError):
             sp.render_tiles(s, integ, 1, pipeline="wavefront")
-
-
-@pytest.mark.parametrize("scene,bvh,w,h", [("bunny.sp", 0, 72, 40), ("material_spheres_ibl.sp", 1, 24, 48),
-                                           ("elf_small.sp", 0, 40, 56)])
-@pytest.mark.parametrize("integrator", ["brute_force_iterative", "brute_force_iterative_rr", "iterative_rrnee"])
-def test_path_wavefront_equals_megakernel(scene_dir, scene, bvh, w, h, integrator):
-    # trace/shade rounds over refilled tile slots (sp_wpath.hip) vs one lane per pixel
-    s = load(scene_dir, scene, w, h, bvh=bvh)
-    m, mst = sp.render_tiles(s, integrator, 5, pipeline="megakernel")
-    v, vst = sp.render_tiles(s, integrator, 5, pipeline="wavefront")
-    assert vst.pipeline == sp.PIPELINES["wavefront"]
-    assert np.array_equal(m.view(np.uint32), v.view(np.uint32)), rel_l2(v, m)
-    assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
-        (vst.rays, vst.shadow_rays, vst.samples, vst.rng_draws)
-
-
-def test_path_wavefront_slot_refill(scene_dir, monkeypatch):
-    # 3 slots for 45 tiles in a shuffled order: every slot is refilled many times
-    s = load(scene_dir, "bunny.sp", 72, 40, bvh=0)
-    ids = np.random.default_rng(5).permutation(sp.TileScheduler(72, 40).get_num_tiles()).astype(np.int32)
-    full, _ = sp.render_tiles(s, "iterative_rrnee", 3, ids, pipeline="wavefront")
-    monkeypatch.setenv("SP_PATH_SLOTS", "3")
-    few, fst = sp.render_tiles(s, "iterative_rrnee", 3, ids, pipeline="wavefront")
-    assert np.array_equal(few.view(np.uint32), full.view(np.uint32))
-    c, cst = _oracle.render(s, 5, 3, ids, variant="spm")
-    assert fst.rays == cst["rays"] and fst.samples == cst["samples"]
-    assert rel_l2(few, c) < REL_L2_TOL
 
 
 @pytest.mark.parametrize("scene,w,h,integrator,spp", [("bunny.sp", 64, 40, "direct_lighting", 4),
@@ -290,26 +225,12 @@ def test_vs_reference_build_bitexact(scene_dir, scene, w, h, integrator, spp):
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), rel_l2(g, r)
 
 
-@pytest.mark.parametrize("integrator", ["brute_force_iterative", "brute_force_iterative_rr", "iterative_rrnee"])
-def test_megakernel_regen_equals_lockstep(scene_dir, monkeypatch, integrator):
-    # per-lane sample regeneration (SP_REGEN=1) vs the lock-step sample loop: same images and counts
-    s = load(scene_dir, "elf_small.sp", 40, 56, bvh=0)
-    monkeypatch.setenv("SP_REGEN", "1")
-    a, ast = sp.render_tiles(s, integrator, 4, pipeline="megakernel")
-    monkeypatch.setenv("SP_REGEN", "0")
-    b, bst = sp.render_tiles(s, integrator, 4, pipeline="megakernel")
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
-    assert (ast.rays, ast.shadow_rays, ast.samples, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.samples, bst.rng_draws)
-
-
 @pytest.mark.parametrize("scene,w,h", [("bunny.sp", 64, 40), ("lucy_small.sp", 40, 56), ("elf_small.sp", 40, 56)])
-def test_wide_bvh_vs_binary(scene_dir, monkeypatch, scene, w, h):
+def test_wide_bvh_vs_binary(scene_dir, scene, w, h):
     # 8-wide quantised BVH (SAH default) vs the binary SAH walk: same rays traced (any-hit is
     # exact, closest hit differs only on exactly equal distances) and the oracle tolerance
-    monkeypatch.setenv("SP_WIDE", "0")
-    s0 = load(scene_dir, scene, w, h, bvh=0)
+    s0 = load(scene_dir, scene, w, h, bvh=0, wide_bvh=False)
     b, bst = sp.render_tiles(s0, "direct_lighting", 4)
-    monkeypatch.setenv("SP_WIDE", "1")
     s1 = load(scene_dir, scene, w, h, bvh=0)
     a, ast = sp.render_tiles(s1, "direct_lighting", 4)
     c, _ = _oracle.render(s1, 6, 4, variant="spm")
@@ -331,7 +252,7 @@ def test_deep_recursion_bitexact(scene_dir, integrator):
 
 @pytest.mark.parametrize("integrator,pipeline", [("direct_lighting", "megakernel"), ("direct_lighting", "wavefront"),
                                                  ("direct_lighting", "chunks"), ("iterative_rrnee", "megakernel"),
-                                                 ("iterative_rrnee", "wavefront"), ("whitted", "megakernel")])
+                                                 ("whitted", "megakernel")])
 def test_degenerate_deep_bvh_stackless_bitexact(scene_dir, integrator, pipeline):
     # a reference BVH 172 levels deep (the reference's recursion is unbounded, BVHAccelerator.h:
     # 62-77): past the LDS budget, so every walk climbs parent links instead of a stack -- same
@@ -350,18 +271,19 @@ def test_degenerate_deep_bvh_stackless_bitexact(scene_dir, integrator, pipeline)
 @pytest.mark.parametrize("scene,w,h", [("bunny.sp", 64, 40), ("lucy_small.sp", 40, 56), ("material_spheres_ibl.sp", 24, 48)])
 @pytest.mark.parametrize("integrator", ["direct_lighting", "iterative_rrnee"])
 def test_forced_stackless_walk(scene_dir, monkeypatch, scene, w, h, integrator):
-    # SP_STACKLESS=1: the parent-link walk on ordinary scenes -- bit-exact vs the oracle on the
-    # reference BVH, and bit-identical to the stack walk on the SAH binary BVH (near-first order)
-    monkeypatch.setenv("SP_STACKLESS", "1")
-    s = load(scene_dir, scene, w, h, bvh=1)
+    # the parent-link walk forced on ordinary scenes (sp_upload_params.walk, and the SP_STACKLESS
+    # test override) -- bit-exact vs the oracle on the reference BVH, and bit-identical to the
+    # stack walk on the SAH binary BVH (near-first order)
+    s = load(scene_dir, scene, w, h, bvh=1, stackless=True)
     g, gst = sp.render_tiles(s, integrator, 3)
     assert gst.stack_depth == 0
     c, _ = _oracle.render(s, sp.string_to_integrator_type(integrator), 3, variant="spm")
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
+    monkeypatch.setenv("SP_STACKLESS", "1")
     a, ast = sp.render_tiles(load(scene_dir, scene, w, h, bvh=0), integrator, 3)
-    monkeypatch.setenv("SP_STACKLESS", "0")
-    monkeypatch.setenv("SP_WIDE", "0")  # the stackless scene walks the binary SAH BVH for any-hit too
-    b, bst = sp.render_tiles(load(scene_dir, scene, w, h, bvh=0), integrator, 3)
+    monkeypatch.delenv("SP_STACKLESS")
+    # the stackless scene walks the binary SAH BVH for any-hit too
+    b, bst = sp.render_tiles(load(scene_dir, scene, w, h, bvh=0, wide_bvh=False), integrator, 3)
     assert ast.stack_depth == 0 and bst.stack_depth > 0
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
     assert (ast.rays, ast.shadow_rays, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.rng_draws)
