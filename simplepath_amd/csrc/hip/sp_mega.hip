@@ -1,19 +1,7 @@
 // sp_mega.hip -- launch helpers of the megakernel (sp_mega.hpp); kernels live in sp_mega_*.hip.
 #include "sp_mega.hpp"
 
-#include <cstdlib>
-
 namespace spd {
-
-// SP_RRNEE_MERGED=1: the lock-step IterativeRRNEE megakernel with the selection-weight estimates
-// merged across call sites (sp_path.hpp integrate_rrnee_merged; identical images).  It won while
-// both forms spilled (440 vs 395 Mrays/s on elf 1024^2 x 16 spp); built without SLP
-// vectorisation the per-call-site form needs no scratch and is faster (479 vs 452).
-static bool rrnee_merged_env()
-{
-    const char* v = std::getenv("SP_RRNEE_MERGED");
-    return v ? std::atoi(v) != 0 : false;
-}
 
 // variant = requested waves per SIMD for __launch_bounds__ (DirectLighting 1..4, IterativeRRNEE 2..4)
 KernelFn select_kernel(int integ, int variant)
@@ -23,7 +11,7 @@ KernelFn select_kernel(int integ, int variant)
     case SP_INTEGRATOR_WHITTED: return mega_recursive(integ);
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE:
     case SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR: return mega_iterative(integ);
-    case SP_INTEGRATOR_ITERATIVE_RRNEE: return mega_rrnee(rrnee_merged_env(), variant);
+    case SP_INTEGRATOR_ITERATIVE_RRNEE: return mega_rrnee(variant);
     case SP_INTEGRATOR_MANDELBROT: return mega_mandelbrot();
     default: return mega_direct(variant);
     }

@@ -8,9 +8,6 @@
 namespace spd {
 
 constexpr int WAVES_PER_BLOCK = 4;
-// IterativeRRNEE with its selection-weight estimates merged across call sites (sp_path.hpp
-// integrate_rrnee_merged): same image, another instantiation of the kernel templates.
-constexpr int INTEG_RRNEE_MERGED = 0x100 | SP_INTEGRATOR_ITERATIVE_RRNEE;
 
 template <int INTEG>
 __device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
@@ -19,7 +16,6 @@ __device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
     else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE) return integrate_iterative<false>(c, ray);
     else if constexpr (INTEG == SP_INTEGRATOR_BRUTE_FORCE_ITERATIVE_RR) return integrate_iterative<true>(c, ray);
     else if constexpr (INTEG == SP_INTEGRATOR_ITERATIVE_RRNEE) return integrate_rrnee(c, ray);
-    else if constexpr (INTEG == INTEG_RRNEE_MERGED) return integrate_rrnee_merged(c, ray);
     else if constexpr (INTEG == SP_INTEGRATOR_WHITTED) return integrate_whitted(c, ray);
     else return integrate_direct(c, ray);
 }
@@ -39,7 +35,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
     for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
 #ifdef SP_WAVE_PROF
-    if (lane < 8) wprof_lds[wave * 8 + lane] = 0;
+    if (lane < 16) wprof_lds[wave * 16 + lane] = 0;
 #endif
     __syncthreads();
     Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
@@ -118,7 +114,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
 #endif
     }
 #ifdef SP_WAVE_PROF
-    if (args.tile_diag && lane < 8) atomicAdd(args.tile_diag + lane, wprof_lds[wave * 8 + lane]);
+    if (args.tile_diag && lane < 16) atomicAdd(args.tile_diag + lane, wprof_lds[wave * 16 + lane]);
 #endif
     unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
     for (int k = 0; k < 4; ++k) {
@@ -131,7 +127,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
 using KernelFn = void (*)(Scene, RenderArgs);
 KernelFn mega_direct(int variant);
 KernelFn mega_iterative(int integ);
-KernelFn mega_rrnee(bool merged, int waves);
+KernelFn mega_rrnee(int waves);
 KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 

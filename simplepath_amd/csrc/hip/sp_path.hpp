@@ -25,10 +25,11 @@ using namespace spm;
 // region's share of wave time and its lane occupancy come out separately.  Regions:
 // 0 = a whole sample (integrate), 1 = the 16-sample glossy rho estimate, 2 = closest-hit queries
 // (camera / extension rays: their entry occupancy is the fraction of paths alive), 3 = shadow and
-// MIS-ray queries.  Written by the first active lane into a per-wave LDS row,
+// MIS-ray queries; the block-served IterativeRRNEE kernel adds 4 = advancing lanes between rounds,
+// 5 = waiting at the post barrier, 6 = serving estimates, 7 = waiting at the result barrier.  Written by the first active lane into a per-wave LDS row,
 // flushed to the render's tile_diag buffer at kernel end (sp_mega.hpp).
 #ifdef SP_WAVE_PROF
-static __shared__ unsigned long long wprof_lds[16 * 8];
+static __shared__ unsigned long long wprof_lds[16 * 16];
 __device__ __forceinline__ void wprof_end(int k, uint64_t t0)
 {
     const uint64_t dt    = __builtin_amdgcn_s_memtime() - t0;
@@ -36,8 +37,8 @@ __device__ __forceinline__ void wprof_end(int k, uint64_t t0)
     const int      first = __ffsll((unsigned long long)m) - 1;
     if ((int)(threadIdx.x & 63) == first) {
         const int w = threadIdx.x >> 6;
-        wprof_lds[w * 8 + 2 * k] += dt;
-        wprof_lds[w * 8 + 2 * k + 1] += dt * (uint64_t)__popcll(m);
+        wprof_lds[w * 16 + 2 * k] += dt;
+        wprof_lds[w * 16 + 2 * k + 1] += dt * (uint64_t)__popcll(m);
     }
 }
 #define SP_WPROF(k, stmt)                                                                                              \
@@ -1554,8 +1555,7 @@ __device__ __forceinline__ MSample lambert_sample(const Material& m, Rng& rng)
 }
 
 // Local-space sample/eval/pdf of a non-clearcoat material (OneSampleMaterial).  The glossy forms
-// are split at the selection-weight estimate: *_w take the weights glossy_weights produced (the
-// merged multi-bounce integrator runs that estimate once for lanes at different call sites).
+// are split at the selection-weight estimate: *_w take the weights glossy_weights produced.
 __device__ __forceinline__ MSample onesample_sample_w(const Material& m, f3 wo, const float w[2], Rng& rng, const Rsq& q)
 {
     const float u   = next1D(rng);
@@ -2111,236 +2111,6 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
         } else {
             break;
         }
-    }
-    return L;
-}
-
-// IntegratorIterativeRRNEE with the selection-weight estimates merged across call sites.
-// A bounce evaluates the glossy lobe's 16-sample albedo estimate (glossy_weights) at up to four
-// places -- material.sample for the path (Integrator.cpp:573), and per light material.eval,
-// material.pdf and material.sample in estimate_direct_mis (:507-516) -- and the lanes of a wave
-// reach them at different times (occluded shadow rays skip two, lambertian materials all four).
-// Here each lane runs its bounce as a small state machine up to its next estimate; then every
-// lane waiting on one runs the SAME single copy of glossy_weights together, and all continue.
-// Each lane draws and computes exactly what integrate_rrnee does, in the same order (bit-identical:
-// tests/test_gpu_parity.py); only which lanes share an instruction changes.
-enum : int {
-    RB_PATH, RB_PATH_W, RB_PATH_DONE,            // material.sample for the path
-    RB_LIGHT, RB_EVAL_W, RB_EVAL_DONE, RB_PDF_W, RB_PDF_DONE, RB_MIS, RB_MIS_W, RB_MIS_DONE, // per light
-    RB_END
-};
-
-// ClearcoatMaterial::sample's scaling of its base's sample (Material.h:723-760)
-__device__ __forceinline__ MSample coat_wrap(const Material& top, float f, const MSample& b)
-{
-    if (b.pdf == 0.0f) return b;
-    MSample s;
-    s.pdf   = (1.0f - f) * b.pdf;
-    s.color = cmul(csub(mkc(1, 1, 1), cscale(top.coat_color, f)), b.color);
-    s.dir   = b.dir;
-    s.props = b.props;
-    return s;
-}
-// ClearcoatMaterial::sample's specular branch
-__device__ __forceinline__ MSample coat_reflect(const Material& top, float f, f3 wo)
-{
-    MSample s;
-    s.dir   = mk(-wo.x, wo.y, -wo.z);
-    s.color = cdivs(cscale(top.coat_color, f), abs_f(s.dir.y));
-    s.pdf   = f;
-    s.props = PROP_SPECULAR | PROP_REFLECTIVE;
-    return s;
-}
-// OneSampleMaterial::eval / pdf of a lambertian-only material (no weight estimate, no draws)
-__device__ __forceinline__ rgb lambert_eval(const Material& m)
-{
-    const float w     = lambert_only_weight(m);
-    const float p     = k_uniform_hemisphere_pdf * w;
-    const float inner = 0.0f + p;
-    rgb         r     = mkc(0, 0, 0);
-    if (p > 0.0f) r = cadd(r, cscale(m.lambert_albedo, balance(p, inner)));
-    return r;
-}
-__device__ __forceinline__ float lambert_pdf(const Material& m)
-{
-    const float w = lambert_only_weight(m);
-    float       p = 0.0f;
-    p += w * k_uniform_hemisphere_pdf;
-    return p;
-}
-
-__device__ __forceinline__ rgb integrate_rrnee_merged(Ctx& c, Ray ray)
-{
-    const Scene& sc         = c.sc;
-    rgb          throughput = mkc(1, 1, 1);
-    rgb          L          = mkc(0, 0, 0);
-    float        tmin = k_ray_epsilon, tmax = k_infinite;
-    constexpr float rr_cut = 0.1f;
-    for (int depth = 0; depth < sc.max_depth; ++depth) {
-        rng_prepare(c.rng);
-        const Query qr = trace(c, ray, tmin, tmax);
-        if (!qr.geom) {
-            if (qr.lh.hit) L = cadd(L, cmul(throughput, light_hit_L(sc, qr.lh, ray.d, c.q)));
-            break;
-        }
-        const f3        next_o = ray_at(ray, qr.is.t);
-        const f3        n      = qr.is.n;
-        const f3        P      = qr.is.p;
-        const f3        nv     = normalize(n, c.q); // the shading frame is rebuilt from it where used
-        const f3        wo_l   = to_onb(onb_of_unit(nv), neg(ray.d));
-        const Material& top    = sc.materials[qr.is.material];
-        const bool      coat   = top.kind == SP_MAT_CLEARCOAT;
-        const Material& base   = coat ? sc.materials[top.base] : top;
-        const bool      glossy = base.kind != SP_MAT_LAMBERTIAN;
-        const float     fc     = coat ? fresnel_dielectric(wo_l.y, 1.0f, top.coat_ior) : 0.0f;
-
-        int     stage = RB_PATH, li = 0;
-        bool    path_ok = false;
-        MSample s, ms;
-        LSample ls;
-        f3      wi_l = mk(0, 0, 0);
-        rgb     beL = mkc(0, 0, 0), Lr = mkc(0, 0, 0); // material.eval x light radiance
-        bool    eval_black = true;
-        float   bp = 0.0f, lcos = 0.0f;
-        float   w[2] = { 0.0f, 0.0f };
-        while (true) {
-            bool need = false;
-            while (!need && stage != RB_END) {
-                // material.sample (path or MIS): the coat's coin, then the base's lobe
-                if (stage == RB_PATH || stage == RB_MIS) {
-                    const bool mis = stage == RB_MIS;
-                    bool       done = false;
-                    MSample    r;
-                    if (coat && next1D(c.rng) < fc) {
-                        r    = coat_reflect(top, fc, wo_l);
-                        done = true;
-                    } else if (glossy) {
-                        need  = true;
-                        stage = mis ? RB_MIS_W : RB_PATH_W;
-                    } else {
-                        r = lambert_sample(base, c.rng);
-                        if (coat) r = coat_wrap(top, fc, r);
-                        done = true;
-                    }
-                    if (done) {
-                        if (mis) ms = r;
-                        else s = r;
-                        stage = mis ? RB_MIS_DONE : RB_PATH_DONE;
-                    }
-                } else if (stage == RB_PATH_W || stage == RB_MIS_W) {
-                    MSample r = onesample_sample_w(base, wo_l, w, c.rng, c.q);
-                    if (coat) r = coat_wrap(top, fc, r);
-                    if (stage == RB_MIS_W) {
-                        ms    = r;
-                        stage = RB_MIS_DONE;
-                    } else {
-                        s     = r;
-                        stage = RB_PATH_DONE;
-                    }
-                } else if (stage == RB_PATH_DONE) { // material_sample's world transform and the path test
-                    if (s.pdf == 0.0f || cblack(s.color)) {
-                        path_ok = false;
-                        stage   = RB_END;
-                    } else {
-                        s.dir   = to_world(onb_of_unit(nv), s.dir);
-                        path_ok = true;
-                        li      = 0;
-                        stage   = RB_LIGHT;
-                    }
-                } else if (stage == RB_LIGHT) { // estimate_direct_mis: light sample, shadow ray
-                    if (li >= sc.n_lights) {
-                        stage = RB_END;
-                        continue;
-                    }
-                    Lr = mkc(0, 0, 0);
-                    const Light& l = sc.lights[li];
-                    ls             = light_sample(sc, l, P, n, next2D(c.rng), c.q);
-                    if (ls.pdf == 0.0f || cblack(ls.L) || occluded(c, ls.ray, ls.tmin, ls.tmax)) {
-                        L = cadd(L, cmul(throughput, Lr));
-                        ++li;
-                        continue;
-                    }
-                    wi_l = to_onb(onb_of_unit(nv), ls.ray.d);
-                    lcos = abs_f(dot(ls.ray.d, n));
-                    if (glossy) {
-                        need  = true;
-                        stage = RB_EVAL_W;
-                    } else {
-                        const rgb be = coat ? cscale(lambert_eval(base), 1.0f - fc) : lambert_eval(base);
-                        eval_black   = cblack(be);
-                        beL          = cmul(be, ls.L);
-                        stage        = RB_EVAL_DONE;
-                    }
-                } else if (stage == RB_EVAL_W) {
-                    const rgb v  = onesample_eval_w(base, wo_l, wi_l, w, c.q);
-                    const rgb be = coat ? cscale(v, 1.0f - fc) : v;
-                    eval_black   = cblack(be);
-                    beL          = cmul(be, ls.L);
-                    stage        = RB_EVAL_DONE;
-                } else if (stage == RB_EVAL_DONE) { // material.pdf when the eval is not black
-                    if (eval_black) {
-                        stage = RB_MIS;
-                    } else if (glossy) {
-                        need  = true;
-                        stage = RB_PDF_W;
-                    } else {
-                        bp    = coat ? (1.0f - fc) * lambert_pdf(base) : lambert_pdf(base);
-                        stage = RB_PDF_DONE;
-                    }
-                } else if (stage == RB_PDF_W) {
-                    const float v = onesample_pdf_w(base, wo_l, wi_l, w, c.q);
-                    bp            = coat ? (1.0f - fc) * v : v;
-                    stage         = RB_PDF_DONE;
-                } else if (stage == RB_PDF_DONE) {
-                    if (bp > 0.0f) {
-                        const float wgt = balance(ls.pdf, ls.pdf + bp);
-                        Lr              = cadd(Lr, cscale(beL, lcos * wgt / ls.pdf));
-                    }
-                    stage = RB_MIS;
-                } else if (stage == RB_MIS_DONE) { // the MIS direction: light pdf, MIS ray
-                    if (!(ms.pdf == 0.0f || cblack(ms.color))) {
-                        ms.dir         = to_world(onb_of_unit(nv), ms.dir);
-                        const Light& l = sc.lights[li];
-                        const float  lp = light_pdf(sc, l, P, ms.dir);
-                        if (lp != 0.0f) {
-                            const float wgt = balance(ms.pdf, ms.pdf + lp);
-                            Ray         mr;
-                            mr.o             = P;
-                            mr.d             = ms.dir;
-                            const float mmin = ray_offset(n, ms.dir);
-                            ++c.rays;
-                            const LightHit lh = scene_intersect_lights(sc, mr, mmin, k_infinite, c.st);
-                            if (lh.hit) {
-                                if (!occluded(c, mr, mmin, k_infinite))
-                                    Lr = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, light_hit_L(sc, lh, mr.d, c.q)),
-                                                                      abs_f(dot(ms.dir, n))), wgt), ms.pdf));
-                            }
-                        }
-                    }
-                    L = cadd(L, cmul(throughput, Lr));
-                    ++li;
-                    stage = RB_LIGHT;
-                }
-            }
-            if (!__any(need)) break;
-            if (need) glossy_weights(base, wo_l, c.rng, c.q, w); // one copy for every call site
-        }
-        if (!path_ok) break;
-        const f3    wi     = s.dir;
-        const float cosine = abs_f(dot(wi, n));
-        throughput         = cmul(throughput, cdivs(cscale(s.color, cosine), s.pdf));
-        if (depth >= sc.rr_depth) {
-            const float lum = luminance(throughput);
-            if (lum < rr_cut) {
-                const float qv = std_max(0.05f, lum / rr_cut);
-                if (next1D(c.rng) < qv) throughput = cdivs(throughput, qv);
-                else break;
-            }
-        }
-        ray.o = next_o;
-        ray.d = wi;
-        tmin  = ray_offset(cosine);
-        tmax  = k_infinite;
     }
     return L;
 }

@@ -287,24 +287,3 @@ def test_forced_stackless_walk(scene_dir, monkeypatch, scene, w, h, integrator):
     assert ast.stack_depth == 0 and bst.stack_depth > 0
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
     assert (ast.rays, ast.shadow_rays, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.rng_draws)
-
-
-@pytest.mark.parametrize("scene,w,h,bvh", [("material_spheres.sp", 24, 48, 1), ("material_spheres_ibl.sp", 24, 48, 1),
-                                           ("bunny.sp", 32, 24, 1), ("elf_small.sp", 40, 56, 1),
-                                           ("wedge_strip.sp", 32, 24, 1), ("elf_small.sp", 40, 56, 0)])
-def test_rrnee_merged_estimates_bitexact(scene_dir, monkeypatch, scene, w, h, bvh):
-    # SP_RRNEE_MERGED=1: IterativeRRNEE with one shared selection-weight estimate per round of
-    # lanes -- every lane's draws and arithmetic as in the reference, so the image, ray counts and
-    # RNG draw counts equal the plain megakernel's (and, on the reference BVH, the oracle's)
-    s = load(scene_dir, scene, w, h, bvh=bvh)
-    monkeypatch.setenv("SP_RRNEE_MERGED", "1")
-    a, ast = sp.render_tiles(s, "iterative_rrnee", 3, pipeline="megakernel")
-    monkeypatch.setenv("SP_RRNEE_MERGED", "0")
-    b, bst = sp.render_tiles(s, "iterative_rrnee", 3, pipeline="megakernel")
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
-    assert (ast.rays, ast.shadow_rays, ast.samples, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.samples, bst.rng_draws)
-    if bvh == 1:
-        c, cst = _oracle.render(s, 5, 3, variant="spm")
-        assert ast.rays == cst["rays"] and ast.shadow_rays == cst["shadow_rays"]
-        assert np.array_equal(a.view(np.uint32), c.view(np.uint32)), rel_l2(a, c)
-

@@ -25,7 +25,7 @@ for n in ${CONFIGS:-spheres bunny_scan bunny_shard2 bunny_shard4 bunny_shard8 lu
   if [ -n "${PMC:-}" ]; then
     sc=$(python -c "import sys;a=sys.argv[1:];print(a[a.index('--scene')+1] if '--scene' in a else 'bunny')" ${A[$n]})
     sw=$(python -c "import sys;a=sys.argv[1:];print(a[a.index('--sim-world')+1] if '--sim-world' in a else 0)" ${A[$n]})
-    SCENE=$sc SIMW=$sw TAG=$n bash tools/gpu_pmc_valu.sh > gpurun_out/cfg/pmc_$n.log 2>&1 || { tail -5 gpurun_out/cfg/pmc_$n.log; exit 1; }
+    SCENE=$sc SIMW=$sw bash tools/gpu_pmc_valu.sh > gpurun_out/cfg/pmc_$n.log 2>&1 || { tail -5 gpurun_out/cfg/pmc_$n.log; exit 1; }
     tail -2 gpurun_out/cfg/pmc_$n.log
   fi
 done

@@ -7,7 +7,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 SCENE=${SCENE:-bunny}
-TAG=${TAG:-$SCENE}
+SIMW=${SIMW:-0}
+if [ "$SIMW" -gt 1 ]; then TAG=${TAG:-${SCENE}_shard$SIMW}; else TAG=${TAG:-$SCENE}; fi
 OUT=gpurun_out/pmcv_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
