@@ -82,13 +82,14 @@ def parse():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
     ap.add_argument("--traffic-json", default=None,
-                    help="tools/pmc_traffic.py output of this workload (default profiles/pmc_bench_<scene>.json)")
+                    help="tools/pmc_traffic.py output of this workload (default profiles/pmc_bench_<scene>[_shard<N>].json)")
     ap.add_argument("--valu-json", default=None,
                     help="tools/pmc_valu.py output of a PMC pass of this workload (VALU-issue roofline; default "
-                         "profiles/pmc_valu_bench_<scene>.json)")
+                         "profiles/pmc_valu_bench_<scene>[_shard<N>].json)")
     a = ap.parse_args()
-    a.traffic_json = a.traffic_json or os.path.join(ROOT, "profiles", f"pmc_bench_{a.scene}.json")
-    a.valu_json = a.valu_json or os.path.join(ROOT, "profiles", f"pmc_valu_bench_{a.scene}.json")
+    tag = a.scene + (f"_shard{a.sim_world}" if a.sim_world > 1 else "")  # tools/gpu_pmc_*.sh output names
+    a.traffic_json = a.traffic_json or os.path.join(ROOT, "profiles", f"pmc_bench_{tag}.json")
+    a.valu_json = a.valu_json or os.path.join(ROOT, "profiles", f"pmc_valu_bench_{tag}.json")
     sc = SCENES[a.scene]
     a.width = a.width or sc["w"]
     a.height = a.height or sc["h"]
@@ -498,8 +499,11 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles, budget_s):
     order = rng.permutation(n_tiles).astype(np.int32)
     ref = _ref_lib()
     ref_scene = None
+    build_s = None
     if ref is not None:  # parse + BVH build outside the timed region, as the reference's main does
+        t_build = time.perf_counter()
         ref_scene = ref.ref_scene_create(scene_path.encode(), args.width, args.height)
+        build_s = time.perf_counter() - t_build
         if not ref_scene:
             ref = None
     kind = "reference" if ref is not None else "port"
@@ -535,6 +539,7 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles, budget_s):
                                              else "oracle liboracle_glibc.so") + ")",
            "msamples_per_s": round(st["samples"] / t_used / 1e6, 5), "host_cores": os.cpu_count(),
            "affinity_cpus": affinity_cpus(),
+           "ref_scene_build_s": None if build_s is None else round(build_s, 2),  # parse + BVH, not timed
            "build": REF_BUILD if ref is not None else "oracle/Makefile: gcc -O2 -mavx2 -mfma -ffp-contract=off"}
     parity = {"vs": kind, "tiles": len(done)}
     if ref is not None:

@@ -31,6 +31,27 @@ namespace spm {
 SP_HD double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 SP_HD double gd(const uint64_t* t, int i) { return u2d(t[i]); }
 
+// The f64 constant with bits B, put in a VGPR pair next to its use.  A polynomial step
+// dfma(r, K1, K2) needs one of its two constants in VGPRs (gfx9 VOP3: one SGPR pair, no f64
+// literal), and left alone the compiler hoists that pair out of every loop: in the DirectLighting
+// megakernel powf's two accumulator constants were held for the whole kernel and, at 128 VGPRs,
+// reloaded from scratch in every sample of the 16-sample rho loop.  The moves take the
+// polynomial's variable as a (never read) operand, so they cannot be hoisted above it; they are
+// ordinary instructions otherwise (not volatile: free to schedule).  The value is the constant.
+template <uint64_t B>
+SP_HD double vk(double dep)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t lo, hi;
+    asm("v_mov_b32 %0, %1 ; %2" : "=v"(lo) : "i"((uint32_t)(B & 0xffffffffull)), "v"(dep));
+    asm("v_mov_b32 %0, %1 ; %2" : "=v"(hi) : "i"((uint32_t)(B >> 32)), "v"(dep));
+    return u2d(((uint64_t)hi << 32) | (uint64_t)lo);
+#else
+    (void)dep;
+    return u2d(B);
+#endif
+}
+
 // Tables read with a per-lane index.  In device code they are served from LDS copies (a
 // 64-lane gather from a global table touches several cache lines per instruction and keeps the
 // vector L1 busy); every kernel that can reach this libm calls libm_lds_init() first.
@@ -91,7 +112,7 @@ SP_HD float lm_expf(float x)
     const double r = dfma(invln2n, xd, -kd);
     uint64_t     t = SPM_EXP2F_T[ki & 31u] + (ki << 47);
     const double s  = u2d(t);
-    const double z  = dfma(r, gd(EXPF_K, 2), gd(EXPF_K, 3));
+    const double z  = dfma(r, gd(EXPF_K, 2), vk<EXPF_K[3]>(r));
     const double r2 = r * r;
     double       y  = dfma(r, gd(EXPF_K, 4), gd(ONE_D, 0));
     y               = dfma(z, r2, y);
@@ -121,7 +142,7 @@ SP_HD float lm_logf(float x)
     const double   r    = dfma(z, invc, gd(MINUS_ONE_D, 0));
     const double   y0   = dfma((double)k, gd(LOGF_K, 0), logc);
     const double   r2   = r * r;
-    double         y    = dfma(r, gd(LOGF_K, 2), gd(LOGF_K, 3));
+    double         y    = dfma(r, gd(LOGF_K, 2), vk<LOGF_K[3]>(r));
     y                   = dfma(r2, gd(LOGF_K, 1), y);
     y                   = dfma(r2, y, r + y0);
     return (float)y;
@@ -182,8 +203,8 @@ SP_HD float lm_powf(float x, float y)
     const double   r    = dfma(z, invc, gd(MINUS_ONE_D, 0));
     const double   y0   = (double)k + logc;
     const double   r2   = r * r;
-    double         yy   = dfma(r, gd(POWF_A, 0), gd(POWF_A, 1));
-    const double   p    = dfma(r, gd(POWF_A, 2), gd(POWF_A, 3));
+    double         yy   = dfma(r, gd(POWF_A, 0), vk<POWF_A[1]>(r));
+    const double   p    = dfma(r, gd(POWF_A, 2), vk<POWF_A[3]>(r));
     const double   r4   = r2 * r2;
     double         q    = dfma(r, gd(POWF_A, 4), y0);
     q                   = dfma(r2, p, q);
@@ -209,7 +230,7 @@ SP_HD float lm_powf(float x, float y)
     const uint64_t ski = ki + sign_bias;
     t += ski << 47;
     const double s   = u2d(t);
-    const double zz  = dfma(rr, gd(EXP2F_K, 1), gd(EXP2F_K, 2));
+    const double zz  = dfma(rr, gd(EXP2F_K, 1), vk<EXP2F_K[2]>(rr));
     const double rr2 = rr * rr;
     double       res = dfma(rr, gd(EXP2F_K, 3), gd(ONE_D, 0));
     res              = dfma(zz, rr2, res);
@@ -231,15 +252,15 @@ SP_HD double sincos_sign(int q) { return (q == 1 || q == 2) ? -1.0 : 1.0; } // s
 SP_HD float sincosf_poly(double x, double x2, int tab, int n)
 {
     if ((n & 1) == 0) {
-        const double s1 = dfma(x2, sc(SC_S3), sc(SC_S2));
+        const double s1 = dfma(x2, sc(SC_S3), vk<glibc::SINCOSF_T[SC_S2]>(x2));
         const double x3 = x2 * x;
         const double x7 = x2 * x3;
         const double s  = dfma(x3, sc(SC_S1), x);
         return (float)dfma(s1, x7, s);
     }
     const double x4 = x2 * x2;
-    const double c1 = dfma(x2, sc(SC_C1), sc(SC_C0));
-    const double c2 = dfma(x2, sc(SC_C4), sc(SC_C3));
+    const double c1 = dfma(x2, sc(SC_C1), vk<glibc::SINCOSF_T[SC_C0]>(x2));
+    const double c2 = dfma(x2, sc(SC_C4), vk<glibc::SINCOSF_T[SC_C3]>(x2));
     const double x6 = x2 * x4;
     const double c  = dfma(x4, sc(SC_C2), c1);
     const float  r  = (float)dfma(c2, x6, c);
