@@ -496,7 +496,7 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles, budget_s):
     n_tiles = sp.TileScheduler(args.width, args.height).get_num_tiles()
     threads = args.cpu_threads if args.cpu_threads > 0 else cpu_share()
     rng = np.random.default_rng(1234)
-    order = rng.permutation(n_tiles).astype(np.int32)
+    order = rng.permutation(np.asarray(my_tiles)).astype(np.int32)  # tiles this GPU rendered (a shard with --sim-world)
     ref = _ref_lib()
     ref_scene = None
     build_s = None
@@ -519,7 +519,7 @@ def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles, budget_s):
         return out
 
     done, t_used, chunk, tiles_out = [], 0.0, threads, []
-    while t_used < budget_s and len(done) < n_tiles:
+    while t_used < budget_s and len(done) < order.size:
         ids = np.ascontiguousarray(order[len(done):len(done) + chunk])
         t0 = time.perf_counter()
         tiles_out.append(run(ids))

@@ -10,8 +10,11 @@
 #include "sp_host.hpp"
 
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <random>
+#include <string>
+#include <vector>
 
 namespace sph {
 
@@ -73,14 +76,20 @@ const RsqrtCapture& rsqrt_capture()
 }
 
 namespace {
-std::mutex   g_override_mu;
-RsqrtCapture g_override;                       // valid when g_use_override
-std::atomic<bool> g_use_override{ false };
+// Installed tables are immutable and never freed (a process installs a handful at most), so a
+// reader's pointer stays valid while another thread installs the next one: no lock on the read
+// path, which runs once per normalize() of every mesh normal while a scene is built.
+std::mutex                               g_override_mu;
+std::vector<std::unique_ptr<RsqrtCapture>> g_installed; // owned for the life of the process
+std::atomic<const RsqrtCapture*>         g_override{ nullptr };
+// Largest table the device copies into LDS next to the traversal stacks: 2 << 13 words (64 KB
+// as 32-bit entries).  Real CPUs need 11 (Intel) or 12 (AMD) bits.
+constexpr int k_max_table_bits = 13;
 } // namespace
 
 const RsqrtCapture& rsqrt_active()
 {
-    if (g_use_override.load(std::memory_order_acquire)) return g_override;
+    if (const RsqrtCapture* o = g_override.load(std::memory_order_acquire)) return *o;
     return rsqrt_capture();
 }
 
@@ -88,24 +97,27 @@ void rsqrt_set_override(const uint32_t* entries, int32_t bits, uint32_t zero_res
 {
     std::lock_guard<std::mutex> lk(g_override_mu);
     if (!entries) {
-        g_use_override.store(false, std::memory_order_release);
+        g_override.store(nullptr, std::memory_order_release);
         return;
     }
-    if (bits < 1 || bits > 23) throw SpError(SP_ERR_ARG, "RSQRTSS table: bits must be 1..23");
-    g_use_override.store(false, std::memory_order_release);
-    g_override.bits          = bits;
-    g_override.entries.assign(entries, entries + (size_t(2) << bits));
-    g_override.zero_result   = zero_result;
-    g_override.denorm_result = denorm_result;
-    g_override.verified      = true; // as given: the table of the CPU that produced the reference
-    g_use_override.store(true, std::memory_order_release);
+    if (bits < 1 || bits > k_max_table_bits)
+        throw SpError(SP_ERR_ARG, "RSQRTSS table: bits must be 1.." + std::to_string(k_max_table_bits) +
+                                      " (2 << bits entries must fit the device's LDS copy)");
+    auto cap           = std::make_unique<RsqrtCapture>();
+    cap->bits          = bits;
+    cap->entries.assign(entries, entries + (size_t(2) << bits));
+    cap->zero_result   = zero_result;
+    cap->denorm_result = denorm_result;
+    cap->verified      = true; // as given: the table of the CPU that produced the reference
+    g_override.store(cap.get(), std::memory_order_release);
+    g_installed.push_back(std::move(cap));
 }
 
 float rsqrtss_active(float a)
 {
-    if (!g_use_override.load(std::memory_order_acquire)) return spm::rsqrtss_host(a);
-    const spm::RsqrtTable t{ g_override.entries.data(), g_override.bits, g_override.zero_result,
-                             g_override.denorm_result };
+    const RsqrtCapture* o = g_override.load(std::memory_order_acquire);
+    if (!o) return spm::rsqrtss_host(a);
+    const spm::RsqrtTable t{ o->entries.data(), o->bits, o->zero_result, o->denorm_result };
     return spm::rsqrtss_emulated(a, t);
 }
 

@@ -72,3 +72,53 @@ def test_rsqrt_table_override_round_trip(scene_dir):
     assert np.array_equal(sp.rsqrt_table()["entries"], t["entries"])
     n3, _ = normals()
     assert np.array_equal(n3.view(np.uint32), base_n.view(np.uint32))
+
+
+def test_rsqrt_table_override_rejects_tables_too_big_for_lds():
+    # 2 << bits entries are copied to LDS by every kernel: more than 13 bits cannot fit next to the
+    # traversal stacks, so sp_rsqrt_table_set refuses it up front with SP_ERR_ARG
+    import simplepath_amd as sp
+    from simplepath_amd import _abi
+
+    big = {"entries": np.zeros(2 << 14, dtype=np.uint32), "bits": 14, "zero_result": 0x7f800000,
+           "denorm_result": 0x7f800000}
+    try:
+        sp.set_rsqrt_table(big)
+        raise AssertionError("expected SP_ERR_ARG")
+    except sp.SimplePathError as e:
+        assert e.code == _abi.SP_ERR_ARG and "LDS" in str(e)
+    finally:
+        sp.set_rsqrt_table(None)
+
+
+def test_rsqrt_table_override_concurrent_readers(scene_dir):
+    # scenes built on one thread while another installs and removes tables: every build sees one
+    # complete table (the override is swapped as a whole, never modified in place)
+    import os
+    import threading
+
+    import simplepath_amd as sp
+
+    path = os.path.join(scene_dir, "bunny.sp")
+    t = sp.rsqrt_table()
+    stop = threading.Event()
+
+    def writer():
+        while not stop.is_set():
+            sp.set_rsqrt_table(t)
+            sp.set_rsqrt_table(None)
+
+    th = threading.Thread(target=writer)
+    th.start()
+    try:
+        base = None
+        for _ in range(6):
+            scene = sp.Scene.from_file(path)  # owns the arrays desc() points into
+            d = scene.desc()
+            n = np.ctypeslib.as_array(d.normals, shape=(d.info.num_vertices, 3)).copy()
+            base = n if base is None else base
+            assert np.array_equal(n.view(np.uint32), base.view(np.uint32))  # same table, either way
+    finally:
+        stop.set()
+        th.join()
+        sp.set_rsqrt_table(None)
