@@ -431,7 +431,8 @@ def roofline_of(stats, pixels, args, kernel_ms):
         achieved = alg / (kernel_ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "ck_camera+ck_count+ck_shade+ck_sum",
-                "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg}
+                "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg,
+                "valu": valu_of(args, "ck_shade")}  # the shading kernel: most of the four kernels' time
     if st.pipeline == 1 or args.integrator != "direct_lighting":  # megakernel, or the sp_wpath rounds
         alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES
         achieved = alg / (kernel_ms * 1e-3) / 1e9
