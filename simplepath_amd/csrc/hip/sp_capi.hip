@@ -19,6 +19,7 @@ namespace spd {
 hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream);
 } // namespace spd
 
 namespace {
@@ -225,6 +226,10 @@ struct sp_scene {
     int32_t*             ck_ctr     = nullptr;
     void*                deep_buf   = nullptr; // recursive integrators beyond MAX_RECURSION levels
     size_t               deep_cap   = 0;
+    float*               d_tile_time = nullptr; // megakernel tile order: probe times, queue order
+    int32_t*             d_order     = nullptr;
+    size_t               order_cap   = 0;
+    unsigned long long*  probe_counters = nullptr;
 
     void release()
     {
@@ -261,6 +266,10 @@ struct sp_scene {
         if (ck_ctr) (void)hipFree(ck_ctr);
         ck_buf = nullptr; ck_ctr = nullptr; ck_cap = 0;
         deep_buf = nullptr; deep_cap = 0;
+        if (d_tile_time) (void)hipFree(d_tile_time);
+        if (d_order) (void)hipFree(d_order);
+        if (probe_counters) (void)hipFree(probe_counters);
+        d_tile_time = nullptr; d_order = nullptr; order_cap = 0; probe_counters = nullptr;
         mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
         ev0 = ev1 = nullptr;
         mt_waves = 0; d_tiles_cap = 0;
@@ -785,14 +794,19 @@ static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params
     if (const char* v = std::getenv("SP_RSQRT_PACK")) // 0: 32-bit entries (comparison)
         if (std::atoi(v) == 0) rs_shift = 0;
     if (rs_shift < 7) rs_shift = 0;
-    if (rs_shift) {
-        std::vector<uint16_t> packed(rc.entries.size());
-        for (size_t i = 0; i < packed.size(); ++i) packed[i] = (uint16_t)((rc.entries[i] & 0x7fffffu) >> rs_shift);
-        const uint16_t* pk = nullptr;
-        up(packed, &pk);
-        d.rsqrt_entries = reinterpret_cast<const uint32_t*>(pk);
-    } else {
-        up(rc.entries, &d.rsqrt_entries);
+    {
+        const uint32_t hdr[spd::RSQ_HDR] = { (uint32_t)rc.bits, rc.zero_result, rc.denorm_result, (uint32_t)rs_shift,
+                                             rs_shift ? rs_hi : 0u, 0u, 0u, 0u };
+        std::vector<uint32_t> words(hdr, hdr + spd::RSQ_HDR);
+        if (rs_shift) {
+            std::vector<uint16_t> packed(rc.entries.size());
+            for (size_t i = 0; i < packed.size(); ++i) packed[i] = (uint16_t)((rc.entries[i] & 0x7fffffu) >> rs_shift);
+            words.resize(spd::RSQ_HDR + (packed.size() + 1) / 2, 0u);
+            std::memcpy(words.data() + spd::RSQ_HDR, packed.data(), packed.size() * sizeof(uint16_t));
+        } else {
+            words.insert(words.end(), rc.entries.begin(), rc.entries.end());
+        }
+        up(words, &d.rsqrt_entries);
     }
     if (rc2 != SP_OK) return rc2;
     d.rsqrt_shift  = rs_shift;
@@ -1228,6 +1242,37 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             SP_HIP(hipMemsetAsync(tdiag, 0, (size_t)n_tiles * 8 * sizeof(unsigned long long), stream));
         }
         a.tile_diag = tdiag;
+        a.order     = nullptr;
+        a.tile_time = nullptr;
+        // Tile order (sp_mega.hip tile_order): a one-sample probe pass times every tile, and the
+        // tiles slower than `hoist` x the mean go to the front of the queue, so the frame does not
+        // end with a few waves finishing expensive tiles alone.  Part of the render (timed with
+        // it); stream-ordered, no host wait.  SP_TILE_HOIST=<factor> (test hook; 0 = queue order).
+        float hoist = 2.0f;
+        if (const char* v = std::getenv("SP_TILE_HOIST")) hoist = (float)std::atof(v);
+        if (hoist > 0.0f && n_tiles > (int64_t)waves) {
+            if ((size_t)n_tiles > s->order_cap) {
+                if (s->d_tile_time) (void)hipFree(s->d_tile_time);
+                if (s->d_order) (void)hipFree(s->d_order);
+                s->d_tile_time = nullptr;
+                s->d_order     = nullptr;
+                s->order_cap   = 0;
+                SP_HIP(hipMalloc(&s->d_tile_time, (size_t)n_tiles * sizeof(float)));
+                SP_HIP(hipMalloc(&s->d_order, (size_t)n_tiles * sizeof(int32_t)));
+                s->order_cap = (size_t)n_tiles;
+            }
+            if (!s->probe_counters) SP_HIP(hipMalloc(&s->probe_counters, 8 * sizeof(unsigned long long)));
+            spd::RenderArgs pr = a;
+            pr.spp       = 1;
+            pr.tile_time = s->d_tile_time;
+            pr.counters  = s->probe_counters; // the probe's rays are not the render's
+            pr.tile_diag = nullptr;
+            SP_HIP(spd::launch_render(s->dev, pr, integ, variant, blocks, lds_bytes, stream));
+            SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, s->d_order, stream));
+            SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
+            a.order = s->d_order;
+            launches += 2;
+        }
         SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
         if (tdiag) { // diagnostic: waits for the render
             SP_HIP(hipStreamSynchronize(stream));
@@ -1239,7 +1284,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                 std::fclose(f);
             }
         }
-        launches = 1;
+        launches += 1;
     }
     SP_HIP(hipEventRecord(s->ev1, stream));
     // stream order: without stats nothing waits -- the render is only enqueued

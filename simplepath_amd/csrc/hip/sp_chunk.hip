@@ -57,7 +57,7 @@ __device__ __forceinline__ Lds lds_setup(const Scene& sc, uint32_t* lds, bool st
     for (int i = tid; i < rs_words; i += 64 * WAVES_PER_BLOCK) lds[i] = sc.rsqrt_entries[i];
     libm_lds_init(tid, 64 * WAVES_PER_BLOCK);
     __syncthreads();
-    Lds l{ Rsq{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi },
+    Lds l{ Rsq{ lds },
            Stack{ lds + rs_words + (stack ? (tid >> 6) * sc.stack_words * 64 : 0), tid & 63, sc.stack_depth } };
     return l;
 }

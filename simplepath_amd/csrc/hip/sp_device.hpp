@@ -122,7 +122,13 @@ struct Scene {
     const uint32_t* light_parents; // parent of each light-BVH node
 };
 // 32-bit words of the RSQRTSS table (the LDS copy every shading kernel makes)
-__host__ __device__ inline int rsqrt_words(const Scene& sc) { return sc.rsqrt_shift ? (1 << sc.rsqrt_bits) : (2 << sc.rsqrt_bits); }
+// RSQRTSS table words on the device: an 8-word header {bits, zero, denorm, shift, hi, 0, 0, 0}
+// then the entries (16-bit packed when shift > 0).  Kernels copy all of it to LDS and read the
+// parameters from the header where they are used (sp_path.hpp rsqrt_ref): held in SGPRs they were
+// spilled to VGPR lanes and read back with v_readlane in every sample of the rho loop (elf
+// 1024^2 @ 16 spp 571-586 -> 600-603 Mrays/s, bunny +1 %, profiles/r03).
+constexpr int RSQ_HDR = 8;
+__host__ __device__ inline int rsqrt_words(const Scene& sc) { return RSQ_HDR + (sc.rsqrt_shift ? (1 << sc.rsqrt_bits) : (2 << sc.rsqrt_bits)); }
 
 
 struct RenderArgs {
@@ -138,6 +144,8 @@ struct RenderArgs {
     float*          deep;       // recursive integrators, max_depth > 32: per-lane level records
     size_t          deep_stride;// lanes of the launch (= blocks * 256)
     unsigned long long* tile_diag; // SP_TILE_DIAG: per slot {t0, t1 (s_memrealtime), wave, item, 4 stage clocks}
+    const int32_t*  order;      // queue position -> tile slot (nullptr: slot order); sp_mega.hip tile_order
+    float*          tile_time;  // probe pass: per slot, the wave's time for the tile; no radiance written
 };
 
 } // namespace spd

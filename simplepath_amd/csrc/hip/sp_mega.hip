@@ -24,6 +24,79 @@ hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int
     return hipGetLastError();
 }
 
+// Tile order for the persistent megakernel.  Each wave renders its tiles one after another, and a
+// tile's cost spans two orders of magnitude (bunny 1080p @ 256 spp: 1 ms of sky to 234 ms of
+// glossy floor under a bunny); in queue order the most expensive tiles can be taken late, and the
+// frame ends with a tail in which a few waves finish them alone (profiles/r03/tile_timeline_*:
+// the last 15 % of the span ran below full occupancy, 9 % of the frame).  A probe pass renders
+// one sample of every tile (sp_render_kernel with spp = 1 and tile_time set: the same code, its
+// radiance discarded; the render re-seeds every pixel's stream) and times each tile; this kernel
+// then moves the tiles whose probe time exceeds `factor` x the mean to the front of the queue.
+// Both classes keep queue order among themselves (a stable partition), so the spatial coherence of
+// consecutive tiles -- which a full longest-first sort loses -- is kept for the rest.
+// Only which wave takes which tile, and when, changes: every pixel's result is the same.
+__global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time, int64_t n, float factor, int32_t* order)
+{
+    __shared__ float s_sum[16];
+    __shared__ int   s_cnt[16], s_ce[16], s_cc[16];
+    __shared__ int   s_base_e, s_base_c;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float     sum = 0.0f;
+    for (int64_t i = tid; i < n; i += 1024) sum += tile_time[i];
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    if (lane == 0) s_sum[wave] = sum;
+    __syncthreads();
+    float total = 0.0f;
+    for (int w = 0; w < 16; ++w) total += s_sum[w];
+    const float thr = factor * total / (float)n;
+    int cnt = 0;
+    for (int64_t i = tid; i < n; i += 1024) cnt += tile_time[i] > thr ? 1 : 0;
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane == 0) s_cnt[wave] = cnt;
+    __syncthreads();
+    if (tid == 0) {
+        int n_exp = 0;
+        for (int w = 0; w < 16; ++w) n_exp += s_cnt[w];
+        s_base_e = 0;
+        s_base_c = n_exp;
+    }
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < n; c0 += 1024) {
+        const int64_t  i  = c0 + tid;
+        const bool     v  = i < n;
+        const bool     e  = v && tile_time[i] > thr;
+        const uint64_t me = __ballot(e), mc = __ballot(v && !e);
+        const uint32_t pe = __builtin_amdgcn_mbcnt_hi((uint32_t)(me >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)me, 0u));
+        const uint32_t pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
+        if (lane == 0) {
+            s_ce[wave] = __popcll(me);
+            s_cc[wave] = __popcll(mc);
+        }
+        __syncthreads();
+        int oe = s_base_e, oc = s_base_c;
+        for (int w = 0; w < wave; ++w) {
+            oe += s_ce[w];
+            oc += s_cc[w];
+        }
+        if (e) order[oe + pe] = (int32_t)i;
+        else if (v) order[oc + pc] = (int32_t)i;
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 0; w < 16; ++w) {
+                s_base_e += s_ce[w];
+                s_base_c += s_cc[w];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream)
+{
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_time, n_tiles, factor, order);
+    return hipGetLastError();
+}
+
 int render_blocks_per_cu(int integ, int variant, size_t lds_bytes)
 {
     int n = 0;

@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
     if (lane < 16) wprof_lds[wave * 16 + lane] = 0;
 #endif
     __syncthreads();
-    Rsq   q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
+    Rsq   q{ lds };
     Stack st{ lds + rs_words + wave * sc.stack_words * 64, lane, sc.stack_depth };
 
     const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;
@@ -53,8 +53,8 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
         const int64_t item = __shfl(grabbed, 0, 64);
         if (item >= args.num_tiles) break;
-        const int64_t  slot    = item;
-        const uint64_t t_start = args.tile_diag ? __builtin_amdgcn_s_memrealtime() : 0;
+        const int64_t  slot    = args.order ? args.order[item] : item;
+        const uint64_t t_start = (args.tile_diag || args.tile_time) ? __builtin_amdgcn_s_memrealtime() : 0;
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
         const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
         const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
@@ -95,6 +95,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
             samples_total += args.spp;
             draws_total += rng.draws;
         }
+        if (args.tile_time) { // probe pass (sp_mega.hip tile_order): how long this tile kept the wave
+            if (lane == 0) args.tile_time[slot] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
+            continue;
+        }
         float* o = args.out + ((size_t)slot * 64 + lane) * 3;
         o[0]     = acc.r;
         o[1]     = acc.g;
@@ -130,5 +134,6 @@ KernelFn mega_iterative(int integ);
 KernelFn mega_rrnee(int waves);
 KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream);
 
 } // namespace spd

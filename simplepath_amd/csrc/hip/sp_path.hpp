@@ -52,17 +52,16 @@ __device__ __forceinline__ void wprof_end(int k, uint64_t t0)
 #endif
 
 // ============================================================================ per-lane state
+// The RSQRTSS table as a kernel holds it (LDS copy, or the global original): t -> the header
+// {bits, zero_result, denorm_result, pack_shift, pack_hi} (sp_device.hpp), entries at t + RSQ_HDR.
 struct Rsq {
     const uint32_t* t;
-    int32_t         bits;
-    uint32_t        zero, denorm;
-    int32_t         shift; // 16-bit entries when > 0 (RsqrtTable::pack_shift)
-    uint32_t        hi;
 };
-
 __device__ __forceinline__ float rsqrt_ref(float a, const Rsq& q)
 {
-    RsqrtTable tb{ q.t, q.bits, q.zero, q.denorm, q.shift, q.hi };
+    const uint4    h  = *reinterpret_cast<const uint4*>(q.t);
+    const uint32_t hi = q.t[4];
+    RsqrtTable     tb{ q.t + RSQ_HDR, (int32_t)h.x, h.y, h.z, (int32_t)h.w, hi };
     return rsqrt_newton(a, rsqrtss_emulated(a, tb));
 }
 __device__ __forceinline__ f3 normalize(f3 a, const Rsq& q) { return scale(a, rsqrt_ref(dot(a, a), q)); }

@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(WF_BLOCK, WF_PRIM_WAVES) wf_primary(Scene sc, 
     float4         hrec = make_float4(0.0f, __uint_as_float(0xffffffffu), 0.0f, 0.0f);
     uint32_t       rays = 0, hits = 0;
     if (pr.inside && sc.max_depth > 0) {
-        const Rsq   q{ sc.rsqrt_entries, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
+        const Rsq   q{ sc.rsqrt_entries };
         const Ray   ray  = camera_ray(sc, pr, sample, q);
         float       tmax = k_infinite;
         const Stack st{ lds + (threadIdx.x >> 6) * sc.stack_words * 64, lane, sc.stack_depth };
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(WF_BLOCK, MINW) wf_shade(Scene sc, WaveArgs w,
 #define SP_STAMP(k) ((void)0)
 #endif
     if (pr.inside) {
-        const Rsq q{ lds, sc.rsqrt_bits, sc.rsqrt_zero, sc.rsqrt_denorm, sc.rsqrt_shift, sc.rsqrt_hi };
+        const Rsq q{ lds };
         Rng       rng = rng_load(w, p);
         rng_prepare(rng);
         SP_STAMP(1);

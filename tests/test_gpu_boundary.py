@@ -142,3 +142,23 @@ def test_upload_options_are_part_of_the_residency(scene_dir):
             assert st.stack_depth == 0
         else:
             assert st.stack_depth == rst.stack_depth
+
+
+@pytest.mark.parametrize("integrator", ["direct_lighting", "iterative_rrnee", "whitted"])
+def test_tile_order_probe_is_invisible(scene_dir, monkeypatch, integrator):
+    # the megakernel's tile order (a one-sample probe pass, then the slow tiles first) changes only
+    # which wave renders which tile and when: images and ray / draw counts equal queue order's,
+    # also for a tile subset in a shuffled order
+    s = load(scene_dir, "bunny.sp", 640, 512)  # 5120 tiles: more than the persistent waves (4096)
+    ref, rst = sp.render_tiles(s, integrator, 2, pipeline="megakernel")
+    assert rst.launches == 3  # probe, partition, render
+    monkeypatch.setenv("SP_TILE_HOIST", "0")
+    off, ost = sp.render_tiles(s, integrator, 2, pipeline="megakernel")
+    assert ost.launches == 1
+    assert np.array_equal(ref.view(np.uint32), off.view(np.uint32))
+    assert (rst.rays, rst.shadow_rays, rst.samples, rst.rng_draws) == (ost.rays, ost.shadow_rays, ost.samples, ost.rng_draws)
+    for factor in ("0.5", "1.0", "4.0"):
+        monkeypatch.setenv("SP_TILE_HOIST", factor)
+        ids = np.random.default_rng(int(float(factor) * 10)).permutation(ref.shape[0]).astype(np.int32)
+        sub, _ = sp.render_tiles(s, integrator, 2, ids, pipeline="megakernel")
+        assert np.array_equal(sub.view(np.uint32), ref[ids].view(np.uint32)), factor

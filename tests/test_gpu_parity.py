@@ -123,7 +123,7 @@ def test_wavefront_equals_megakernel(scene_dir, scene, bvh):
     assert np.array_equal(m.view(np.uint32), w.view(np.uint32)), rel_l2(w, m)
     assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
         (wst.rays, wst.shadow_rays, wst.samples, wst.rng_draws)
-    assert wst.launches == 3 + 4 * 5 and mst.launches == 1
+    assert wst.launches == 3 + 4 * 5 and mst.launches in (1, 3)  # 3: tile-order probe + partition + render
 
 
 @pytest.mark.parametrize("scene,bvh,chunks,replay", [("bunny.sp", 0, "0", "0"), ("bunny.sp", 1, "3", "0"),
