@@ -1247,8 +1247,12 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // Tile order (sp_mega.hip tile_order): a one-sample probe pass times every tile, and the
         // tiles slower than `hoist` x the mean go to the front of the queue, so the frame does not
         // end with a few waves finishing expensive tiles alone.  Part of the render (timed with
-        // it); stream-ordered, no host wait.  SP_TILE_HOIST=<factor> (test hook; 0 = queue order).
-        float hoist = 2.0f;
+        // it); stream-ordered, no host wait.  Used where it measured faster (profiles/r03/
+        // ab_tile_order.txt): many tiles per persistent wave and a probe that costs little of the
+        // frame -- bunny 1080p @ 256 spp (7.9 tiles per wave) +3-4 %, lucy +2 %, elf's 8-way
+        // shard +3 %; spheres 1024^2 (4 tiles per wave) lost 1 % at 256 spp and 5 % at 64 spp.
+        // SP_TILE_HOIST=<factor> forces it (test hook; 0 = queue order).
+        float hoist = (n_tiles >= 6 * (int64_t)waves && p->samples_per_pixel >= 128) ? 2.0f : 0.0f;
         if (const char* v = std::getenv("SP_TILE_HOIST")) hoist = (float)std::atof(v);
         if (hoist > 0.0f && n_tiles > (int64_t)waves) {
             if ((size_t)n_tiles > s->order_cap) {
@@ -1263,7 +1267,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             }
             if (!s->probe_counters) SP_HIP(hipMalloc(&s->probe_counters, 8 * sizeof(unsigned long long)));
             spd::RenderArgs pr = a;
-            pr.spp       = 1;
+            pr.spp       = 1; // 2 or 4 probe samples measured no better (profiles/r03/ab_tile_order.txt)
             pr.tile_time = s->d_tile_time;
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;

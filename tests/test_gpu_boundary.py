@@ -150,6 +150,7 @@ def test_tile_order_probe_is_invisible(scene_dir, monkeypatch, integrator):
     # which wave renders which tile and when: images and ray / draw counts equal queue order's,
     # also for a tile subset in a shuffled order
     s = load(scene_dir, "bunny.sp", 640, 512)  # 5120 tiles: more than the persistent waves (4096)
+    monkeypatch.setenv("SP_TILE_HOIST", "2")    # forced: AUTO uses it from 6 tiles per wave and 128 spp
     ref, rst = sp.render_tiles(s, integrator, 2, pipeline="megakernel")
     assert rst.launches == 3  # probe, partition, render
     monkeypatch.setenv("SP_TILE_HOIST", "0")
