@@ -79,6 +79,8 @@ def parse():
                     help="test hook: spawn the ranks like --gpus N does, join a gloo group, no GPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront", "chunks"])
+    ap.add_argument("--waves", type=int, default=0,
+                    help="megakernel occupancy variant (sp_render_params.waves_per_simd; 0 = automatic)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
     ap.add_argument("--traffic-json", default=None,
@@ -240,7 +242,7 @@ def main():
             out[: len(my_tiles)] = torch.from_numpy(tiles)
             return _CpuStats(st, (time.perf_counter() - t) * 1e3)
         return sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
-                                      pipeline=args.pipeline, stage_timing=True)
+                                      pipeline=args.pipeline, stage_timing=True, waves_per_simd=args.waves)
 
     def step():
         st = render()
