@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cctype>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -626,9 +627,9 @@ private:
         c.pos = start;
         while (true) {
             const std::string w = c.token();
+            const size_t at = c.pos; // tellg() right after the token, before `>> c` skips blanks
             c.skip_ws();
             if (c.eof()) break;
-            const size_t at = c.pos;
             if (c.get_char() != '{') parse_error(on_line("Expected '{' character", at));
             const size_t close = clean.find('}', c.pos);
             const std::string body = clean.substr(c.pos, close == std::string::npos ? std::string::npos : close - c.pos);
@@ -662,25 +663,33 @@ private:
         Cursor       c(body);
         while (true) {
             const std::string w = c.token();
+            const size_t at = body_off + c.pos; // consume_character's line: tellg() before `>> c`
             c.skip_ws();
             if (c.eof() || c.fail) break;
-            if (c.get_char() != ':') parse_error(on_line("Expected ':' character", body_off + c.pos));
+            if (c.get_char() != ':') parse_error(on_line("Expected ':' character", at));
             if (!fn(w, c)) parse_error(on_line(std::string("Unknown ") + what + " attribute: " + w, body_off + c.pos));
             if (c.fail) break; // a failed extraction stops the reference's loop as well
         }
     }
 
+    // m_materials.find + LOG_ERROR (base/FileParser.cpp:494-498, 555-559): an unknown name is
+    // reported and parsing goes on; the block's own check ("needs a base material" / "needs a
+    // material") then fails
     int find_material(const std::string& name)
     {
         for (size_t i = 0; i < m_scene->material_names.size(); ++i)
             if (m_scene->material_names[i] == name) return static_cast<int>(i);
-        throw SpError(SP_ERR_PARSE, "Material '" + name + "' not found");
+        std::fprintf(stderr, "Material '%s' not found\n", name.c_str());
+        return -1;
     }
+    // the checks after a block's attribute loop (base/FileParser.cpp:408-416): the loop only ends
+    // with the stream failed, so tellg() is -1 and the line is that of offset-1, the block's '{'
+    std::string at_block_end(const std::string& what) const { return on_line(what, m_body_off - 1); }
     void add_material(const std::string& name, const sp_material_desc& d)
     {
-        if (name.empty()) parse_error("Material needs named");
+        if (name.empty()) parse_error(at_block_end("Material needs named"));
         for (auto& n : m_scene->material_names)
-            if (n == name) parse_error("Material " + name + " already exists");
+            if (n == name) parse_error(at_block_end("Material " + name + " already exists"));
         m_scene->material_names.push_back(name);
         m_scene->materials.push_back(Material{ d });
     }
@@ -807,8 +816,8 @@ private:
             else return false;
             return true;
         });
-        if (name.empty()) parse_error("Material needs named");
-        if (base < 0) parse_error("Clearcoat material needs a base material");
+        if (name.empty()) parse_error(at_block_end("Material needs named"));
+        if (base < 0) parse_error(at_block_end("Clearcoat material needs a base material"));
         sp_material_desc d = blank_material();
         d.kind             = SP_MAT_CLEARCOAT;
         d.base             = base;
