@@ -227,11 +227,13 @@ typedef struct sp_upload_params {
     int32_t walk;             /* SP_WALK_AUTO: per-wave LDS stack unless the BVH is deeper than
                                  stack_max_levels; SP_WALK_STACKLESS: parent links always         */
     int32_t stack_max_levels; /* 0 = 96                                                            */
-    int32_t no_wide_bvh;      /* 1: any-hit queries walk the binary BVH instead of the 8-wide one   */
+    int32_t no_wide_bvh;      /* 1: all queries walk the binary BVH instead of the 8-wide one       */
     int32_t env_replay;       /* 1: image-light CDF lookups replay libstdc++ upper_bound step by step
                                  instead of the guide tables (identical results)                    */
     int32_t sah_leaf;         /* SAH leaf size 1-4: 0 = 4                                          */
-    int32_t reserved[2];      /* must be 0                                                          */
+    int32_t binary_closest;   /* 1: closest-hit queries keep the binary near-first walk (any-hit
+                                 queries stay on the 8-wide BVH)                                    */
+    int32_t reserved;         /* must be 0                                                          */
 } sp_upload_params;
 
 typedef struct sp_render_stats {

@@ -114,16 +114,19 @@ class Scene:
         check(lib().sp_scene_set_resolution(self._h, width, height))
 
     def upload(self, device: int = 0, bvh_mode: int = 0, stackless: bool = False, stack_max_levels: int = 0,
-               wide_bvh: bool = True, env_replay: bool = False, sah_leaf: int = 0) -> None:
+               wide_bvh: bool = True, env_replay: bool = False, sah_leaf: int = 0,
+               binary_closest: bool = False) -> None:
         """bvh_mode 0 = SAH (throughput), 1 = the reference's median-split BVH (tie-exact order).
         The other options (sp_upload_params) change how the same image is computed, never the
-        image: the parent-link walk, the LDS-stack depth budget, the 8-wide any-hit BVH, the
-        image-light guide tables, the SAH leaf size."""
+        image: the parent-link walk, the LDS-stack depth budget, the image-light guide tables, the
+        SAH leaf size.  On the SAH BVH, wide_bvh / binary_closest choose the 8-wide or binary walks,
+        which can only differ in which of two primitives at exactly equal distance wins."""
         p = _abi.sp_upload_params()
         p.bvh_mode = bvh_mode
         p.walk = _abi.SP_WALK_STACKLESS if stackless else _abi.SP_WALK_AUTO
         p.stack_max_levels = stack_max_levels
         p.no_wide_bvh = 0 if wide_bvh else 1
+        p.binary_closest = 1 if binary_closest else 0
         p.env_replay = 1 if env_replay else 0
         p.sah_leaf = sah_leaf
         check(lib().sp_scene_upload_ex(self._h, device, C.byref(p)))

@@ -104,7 +104,7 @@ SP_WALK_AUTO, SP_WALK_STACKLESS = 0, 1
 class sp_upload_params(C.Structure):
     _fields_ = [("bvh_mode", C.c_int32), ("walk", C.c_int32), ("stack_max_levels", C.c_int32),
                 ("no_wide_bvh", C.c_int32), ("env_replay", C.c_int32), ("sah_leaf", C.c_int32),
-                ("reserved", C.c_int32 * 2)]
+                ("binary_closest", C.c_int32), ("reserved", C.c_int32)]
 
 
 class sp_render_stats(C.Structure):

@@ -102,11 +102,12 @@ struct UploadOpts {
     int  stack_max  = 96;    // deepest BVH (levels) walked with the LDS stack
     bool wide       = true;  // 8-wide any-hit BVH on SAH scenes
     bool env_guide  = true;  // image-light guide tables
+    bool wide_closest = true;  // closest-hit queries on the 8-wide BVH as well
     int  sah_leaf   = 4;
     bool operator==(const UploadOpts& o) const
     {
         return bvh_mode == o.bvh_mode && stackless == o.stackless && stack_max == o.stack_max && wide == o.wide &&
-               env_guide == o.env_guide && sah_leaf == o.sah_leaf;
+               env_guide == o.env_guide && sah_leaf == o.sah_leaf && wide_closest == o.wide_closest;
     }
 };
 
@@ -120,8 +121,8 @@ int resolve_upload(const sp_upload_params* p, UploadOpts& o)
 {
     const sp_upload_params z{};
     if (!p) p = &z;
-    for (int32_t r : p->reserved)
-        if (r != 0) return fail(SP_ERR_ARG, "sp_upload_params.reserved must be 0");
+    if (p->reserved != 0) return fail(SP_ERR_ARG, "sp_upload_params.reserved must be 0");
+    if (p->binary_closest != 0 && p->binary_closest != 1) return fail(SP_ERR_ARG, "binary_closest must be 0 or 1");
     if (p->bvh_mode != 0 && p->bvh_mode != 1) return fail(SP_ERR_ARG, "bvh_mode must be 0 (SAH) or 1 (reference)");
     if (p->walk != SP_WALK_AUTO && p->walk != SP_WALK_STACKLESS) return fail(SP_ERR_ARG, "walk must be SP_WALK_AUTO or SP_WALK_STACKLESS");
     if (p->stack_max_levels < 0) return fail(SP_ERR_ARG, "stack_max_levels < 0");
@@ -131,6 +132,7 @@ int resolve_upload(const sp_upload_params* p, UploadOpts& o)
     o.stack_max = p->stack_max_levels ? p->stack_max_levels : std::max(1, env_int("SP_STACK_MAX", 96));
     o.wide      = !p->no_wide_bvh && env_int("SP_WIDE", 1) != 0;
     o.env_guide = !p->env_replay && env_int("SP_ENV_GUIDE", 1) != 0;
+    o.wide_closest = !p->binary_closest && env_int("SP_WIDE_CLOSEST", 1) != 0;
     // SAH leaf size limit (1..4: 8 collapsed leaves of a wide node must fit its 5-bit leaf
     // offsets; the sweep in DESIGN.md §4 found 4 best)
     o.sah_leaf  = p->sah_leaf ? p->sah_leaf : std::max(1, std::min(4, env_int("SP_SAH_LEAF", 4)));
@@ -818,11 +820,14 @@ static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params
     s->light_depth = lbvh.max_depth;
     s->geom_nodes  = nodes.size();
     s->geom_slots  = slot_code.size();
-    // Any-hit queries walk the 8-wide BVH; closest-hit queries keep the binary near-first walk
-    // (coherent camera rays: binary 0.48 vs wide 0.69 ms per primary launch on the bunny frame,
-    // while shadow rays gain 0.82 -> 0.53 ms).
+    // SAH scenes walk the 8-wide BVH for every query: any-hit since round 1 (shadow stage 0.82 ->
+    // 0.53 ms), closest hit since round 3 with octant-ordered slots, near-first entry and group
+    // distances (bunny 3110 -> 3200, lucy 2175 -> 2280 Mrays/s).  Its stack keeps a
+    // distance per entry in the upper half.
     d.ordered     = bvh_mode == 1 ? 0 : 1; // reference order is part of the bit-exact contract
-    d.stack_depth = std::max(bvh.max_depth, std::max(wide.depth, lbvh.max_depth)) + 1;
+    d.wide_closest = (opts.wide_closest && !wide.words.empty()) ? 1 : 0;
+    d.stack_depth  = std::max(bvh.max_depth, std::max(wide.depth, lbvh.max_depth)) + 1;
+    if (d.wide_closest) d.stack_depth = std::max(d.stack_depth, 2 * (wide.depth + 1)); // + group distances
     d.stackless   = stackless ? 1 : 0;
     d.parents       = nullptr;
     d.light_parents = nullptr;
@@ -1412,6 +1417,7 @@ int sp_scene_bvh_build_info(const sp_scene* s, int32_t bvh_mode, sp_bvh_info* ou
         const bool stackless       = stackless_for(opts, std::max(out->depth, out->light_depth));
         if (wide_enabled(opts) && !bvh.nodes.empty() && !stackless) out->wide_depth = sph::build_wide(bvh).depth;
         out->stack_depth = stackless ? 0 : std::max(out->depth, std::max(out->wide_depth, out->light_depth)) + 1;
+        if (out->wide_depth && opts.wide_closest) out->stack_depth = std::max(out->stack_depth, 2 * (out->wide_depth + 1));
         return SP_OK;
     } catch (const std::exception& e) {
         return fail(SP_ERR_UNSUPPORTED, std::string("BVH build failed: ") + e.what());

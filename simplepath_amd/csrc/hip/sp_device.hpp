@@ -115,6 +115,7 @@ struct Scene {
     // stack entries, usually far fewer than stack_words (which covers the binary closest-hit walk)
     int             any_stack_words;
     int             ordered;       // 1: SAH BVH -- visit the near child (split axis, ray sign) first
+    int             wide_closest;  // 1: closest-hit queries walk the 8-wide BVH too (stack: 2 words per level)
     // BVHs too deep for the LDS stack budget: binary walks climb parent links instead of popping
     // a stack (same visiting order and box tests; sp_path.hpp bvh_next)
     int             stackless;

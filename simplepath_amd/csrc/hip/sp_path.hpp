@@ -615,6 +615,7 @@ __device__ __forceinline__ float ubyte(uint32_t w, int k) { return (float)((w >>
 struct WideHits {
     uint32_t inner, leaf; // slot masks
     int      nearest;     // inner slot with the smallest entry distance
+    float    t_rest;      // smallest entry distance of the other hit inner slots
     uint32_t child_base, leaf_base, meta_lo, meta_hi;
 };
 __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, const Ray& ray, const f3& inv, float tmin,
@@ -628,7 +629,7 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
     const float    sz = __uint_as_float(((w0.w >> 16) & 0xffu) << 23);
     const uint32_t imask = w0.w >> 24;
     WideHits       r;
-    r.inner = 0; r.leaf = 0; r.nearest = -1;
+    r.inner = 0; r.leaf = 0; r.nearest = -1; r.t_rest = k_infinite;
     r.child_base = w1.x; r.leaf_base = w1.y; r.meta_lo = w1.z; r.meta_hi = w1.w;
     float best = k_infinite;
 #pragma unroll
@@ -648,7 +649,8 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
         if (!wbox(lx, ly, lz, hx, hy, hz, ray, inv, tmin, tmax, t0)) continue;
         if (inner) {
             r.inner |= 1u << k;
-            if (t0 < best) { best = t0; r.nearest = k; }
+            if (t0 < best) { r.t_rest = best; best = t0; r.nearest = k; }
+            else r.t_rest = std_min(r.t_rest, t0);
         } else {
             r.leaf |= 1u << k;
         }
@@ -656,11 +658,13 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
     return r;
 }
 
+__device__ __forceinline__ uint32_t key_mask(uint32_t m, uint32_t o);
 __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
-    const f3 inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    int      sp   = 0;
-    uint32_t node = 0;
+    const f3       inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    const uint32_t o   = dir_sign_bits(ray.d);
+    int            sp  = 0;
+    uint32_t       node = 0;
     while (true) {
         const WideHits wh = wide_visit(sc, node, ray, inv, tmin, tmax);
         for (uint32_t m = wh.leaf; m; m &= m - 1) {
@@ -671,7 +675,7 @@ __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float 
                 if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) return true;
         }
         if (wh.inner) {
-            const uint32_t rest = wh.inner & ~(1u << wh.nearest);
+            const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o); // octant order
             if (rest) {
                 st.s[sp * 64 + st.lane] = (wh.child_base << 8) | rest;
                 ++sp;
@@ -686,9 +690,68 @@ __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float 
         m &= m - 1;
         if (m) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | m;
         else --sp;
-        node = (e >> 8) + (uint32_t)k;
+        node = (e >> 8) + ((uint32_t)k ^ o);
     }
     return false;
+}
+
+// An 8-bit slot mask in visiting order for a ray with direction sign bits o: bit k of the result
+// is slot k ^ o (sp_bvh.cpp places children by octant, so key order is roughly near to far).
+__device__ __forceinline__ uint32_t key_mask(uint32_t m, uint32_t o)
+{
+    m = (o & 1u) ? (((m & 0x55u) << 1) | ((m >> 1) & 0x55u)) : m;
+    m = (o & 2u) ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
+    m = (o & 4u) ? (((m & 0x0fu) << 4) | ((m >> 4) & 0x0fu)) : m;
+    return m;
+}
+
+// Closest hit over the 8-wide BVH: at each node the hit leaves' primitives are tested, the
+// nearest hit inner child is entered and the other hit inner children are pushed as one group
+// entry {child_base << 8 | key mask} with the group's smallest entry distance in the stack's
+// upper half (s[(e + depth / 2) * 64 + lane]; the upload sizes the stack for it); a group whose distance exceeds the closest hit found since is
+// dropped whole.  Every primitive whose (outward-rounded) box meets [tmin, t_closest] is tested,
+// so the result is the binary walk's except which of two primitives at exactly equal t wins.
+__device__ __forceinline__ Hit wide_closest(const Scene& sc, const Ray& ray, float tmin, Hit h, Stack st)
+{
+    const f3       inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    const uint32_t o   = dir_sign_bits(ray.d);
+    const int      half = st.depth >> 1;
+    int            sp   = 0;
+    uint32_t       node = 0;
+    while (true) {
+        const WideHits wh = wide_visit(sc, node, ray, inv, tmin, h.t);
+        for (uint32_t m = wh.leaf; m; m &= m - 1) {
+            const int      k    = __ffs(m) - 1;
+            const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
+            const uint32_t base = wh.leaf_base + (meta & 31u);
+            for (uint32_t j = 0; j < (meta >> 5); ++j) prim_closest(sc, base + j, ray, tmin, h, sc.wslot_tri);
+        }
+        if (wh.inner) {
+            const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o);
+            if (rest) {
+                st.s[sp * 64 + st.lane]              = (wh.child_base << 8) | rest;
+                st.s[(sp + half) * 64 + st.lane]    = __float_as_uint(wh.t_rest);
+                ++sp;
+            }
+            node = wh.child_base + (uint32_t)wh.nearest;
+            continue;
+        }
+        bool found = false;
+        while (sp > 0) {
+            const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
+            if (__uint_as_float(st.s[(sp - 1 + half) * 64 + st.lane]) > h.t) { --sp; continue; }
+            uint32_t  m = e & 0xffu;
+            const int k = __ffs(m) - 1;
+            m &= m - 1;
+            if (m) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | m;
+            else --sp;
+            node  = (e >> 8) + ((uint32_t)k ^ o);
+            found = true;
+            break;
+        }
+        if (!found) break;
+    }
+    return h;
 }
 
 // Wave-uniform record fetch through the constant address space: with the address in SGPRs
@@ -797,6 +860,7 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
         if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
     if (sc.n_nodes == 0) return h;
+    if (sc.wide_closest) return wide_closest(sc, ray, tmin, h, st);
     return sc.stackless ? bvh_closest<true>(sc, ray, tmin, h, st) : bvh_closest<false>(sc, ray, tmin, h, st);
 }
 

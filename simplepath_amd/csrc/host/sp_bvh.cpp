@@ -7,6 +7,7 @@
 // SAH (Wald 2007) with the same node format; it changes only the visiting order.
 #include "sp_host.hpp"
 
+#include <cstdio>
 #include <cstdlib>
 
 #include <stdexcept>
@@ -309,40 +310,69 @@ struct WideBuilder {
             kids[(size_t)best] = left(n);
             kids.insert(kids.begin() + best + 1, right(n));
         }
-        std::vector<uint32_t> inner, leaves;
-        for (uint32_t k : kids) (is_leaf(k) ? leaves : inner).push_back(k);
-        std::vector<uint32_t> order(inner);
-        order.insert(order.end(), leaves.begin(), leaves.end());
-        const int n = (int)order.size();
-        float     lo[3][8], hi[3][8], ulo[3], uhi[3];
+        // Slots by octant: slot s takes the child lying towards (+ on axis a iff bit a of s) from
+        // the node's centre, so a ray whose direction has sign bits o (bit a: d_a < 0) meets the
+        // children roughly near to far in the order slot ^ o = 0, 1, ... (sp_path.hpp key_mask).
+        // Greedy assignment of the largest projection first; inner child in slot s is node
+        // child_base + s (slots taken by leaves or empty leave holes).
+        const int n = (int)kids.size();
+        float     ulo[3], uhi[3], cen[8][3];
         for (int a = 0; a < 3; ++a) { ulo[a] = INFINITY; uhi[a] = -INFINITY; }
         for (int c = 0; c < n; ++c)
             for (int a = 0; a < 3; ++a) {
-                lo[a][c] = b.nodes[order[(size_t)c]].lo[a];
-                hi[a][c] = b.nodes[order[(size_t)c]].hi[a];
-                ulo[a]   = std::min(ulo[a], lo[a][c]);
-                uhi[a]   = std::max(uhi[a], hi[a][c]);
+                ulo[a]    = std::min(ulo[a], b.nodes[kids[(size_t)c]].lo[a]);
+                uhi[a]    = std::max(uhi[a], b.nodes[kids[(size_t)c]].hi[a]);
+                cen[c][a] = 0.5f * (b.nodes[kids[(size_t)c]].lo[a] + b.nodes[kids[(size_t)c]].hi[a]);
+            }
+        int  slot_kid[8];
+        bool kid_done[8] = {};
+        for (int s = 0; s < 8; ++s) slot_kid[s] = -1;
+        for (int round = 0; round < n; ++round) {
+            int   bc = -1, bs = -1;
+            float best = -INFINITY;
+            for (int c = 0; c < n; ++c) {
+                if (kid_done[c]) continue;
+                for (int s = 0; s < 8; ++s) {
+                    if (slot_kid[s] >= 0) continue;
+                    float score = 0.0f;
+                    for (int a = 0; a < 3; ++a) score += ((s >> a) & 1 ? 1.0f : -1.0f) * (cen[c][a] - 0.5f * (ulo[a] + uhi[a]));
+                    if (bc < 0 || score > best) { best = score; bc = c; bs = s; } // NaN (empty box): any slot
+                }
+            }
+            slot_kid[bs] = bc;
+            kid_done[bc] = true;
+        }
+        float lo[3][8], hi[3][8];
+        for (int s = 0; s < 8; ++s)
+            for (int a = 0; a < 3; ++a) {
+                const int c = slot_kid[s] >= 0 ? slot_kid[s] : 0; // empty slots: any box (never tested)
+                lo[a][s]    = b.nodes[kids[(size_t)c]].lo[a];
+                hi[a][s]    = b.nodes[kids[(size_t)c]].hi[a];
             }
         uint8_t q[6][8] = {};
         uint8_t eb[3];
-        for (int a = 0; a < 3; ++a) quantise(lo[a], hi[a], n, ulo[a], uhi[a] - ulo[a], q[a], q[3 + a], eb[a]);
+        for (int a = 0; a < 3; ++a) quantise(lo[a], hi[a], 8, ulo[a], uhi[a] - ulo[a], q[a], q[3 + a], eb[a]);
+        uint32_t imask = 0;
+        int      span  = 0; // child slots allocated: last inner slot + 1
+        for (int s = 0; s < 8; ++s)
+            if (slot_kid[s] >= 0 && !is_leaf(kids[(size_t)slot_kid[s]])) { imask |= 1u << s; span = s + 1; }
         const uint32_t child_base = (uint32_t)(out.words.size() / 20);
-        out.words.resize(out.words.size() + 20 * inner.size());
+        out.words.resize(out.words.size() + 20 * (size_t)span);
         const uint32_t leaf_base = (uint32_t)out.slot_of.size();
         uint8_t        meta[8]   = {};
-        for (int c = (int)inner.size(); c < n; ++c) {
-            const BvhNode& lf  = b.nodes[order[(size_t)c]];
+        for (int s = 0; s < 8; ++s) {
+            if (slot_kid[s] < 0 || ((imask >> s) & 1u)) continue;
+            const BvhNode& lf  = b.nodes[kids[(size_t)slot_kid[s]]];
             const uint32_t cnt = lf.b & ~BVH_LEAF;
             const uint32_t off = (uint32_t)out.slot_of.size() - leaf_base;
             if (cnt == 0 || cnt > 7 || off > 31) throw std::runtime_error("wide BVH: leaf does not fit a meta byte");
-            meta[c] = (uint8_t)(cnt << 5 | off);
+            meta[s] = (uint8_t)(cnt << 5 | off);
             for (uint32_t j = 0; j < cnt; ++j) out.slot_of.push_back((int32_t)(lf.a + j));
         }
         uint32_t* w = &out.words[(size_t)wi * 20];
         std::memcpy(&w[0], &ulo[0], 4);
         std::memcpy(&w[1], &ulo[1], 4);
         std::memcpy(&w[2], &ulo[2], 4);
-        const uint32_t imask = (1u << inner.size()) - 1u;
         w[3] = (uint32_t)eb[0] | (uint32_t)eb[1] << 8 | (uint32_t)eb[2] << 16 | imask << 24;
         w[4] = child_base;
         w[5] = leaf_base;
@@ -352,7 +382,8 @@ struct WideBuilder {
             for (int h = 0; h < 2; ++h)
                 w[8 + 2 * r + h] = (uint32_t)q[r][4 * h] | (uint32_t)q[r][4 * h + 1] << 8 | (uint32_t)q[r][4 * h + 2] << 16 |
                                    (uint32_t)q[r][4 * h + 3] << 24;
-        for (size_t i = 0; i < inner.size(); ++i) emit(child_base + (uint32_t)i, inner[i], depth + 1);
+        for (int s = 0; s < 8; ++s)
+            if ((imask >> s) & 1u) emit(child_base + (uint32_t)s, kids[(size_t)slot_kid[s]], depth + 1);
     }
 };
 
@@ -365,6 +396,9 @@ WideBvh build_wide(const Bvh& bvh)
     out.words.resize(20);
     WideBuilder wb{ bvh, out };
     wb.emit(0, 0, 1);
+    if (out.words.size() / 20 >= (1u << 24)) throw std::runtime_error("wide BVH: more than 2^24 nodes");
+    if (std::getenv("SP_WIDE_STATS"))
+        std::fprintf(stderr, "wide BVH: %zu node records, %zu leaf slots, depth %d\n", out.words.size() / 20, out.slot_of.size(), out.depth);
     return out;
 }
 

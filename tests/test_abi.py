@@ -67,10 +67,10 @@ def test_upload_params_validated_before_the_device(scene_dir):
     # argument errors come back as SP_ERR_ARG before any device is touched (this container has none)
     import ctypes as C
     scene = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp"))
-    for field, value in (("walk", 7), ("bvh_mode", 2), ("sah_leaf", 9), ("stack_max_levels", -1)):
+    for field, value in (("walk", 7), ("bvh_mode", 2), ("sah_leaf", 9), ("stack_max_levels", -1), ("binary_closest", 2)):
         p = _abi.sp_upload_params()
         setattr(p, field, value)
         assert _abi.lib().sp_scene_upload_ex(scene.handle, 0, C.byref(p)) == _abi.SP_ERR_ARG, field
     p = _abi.sp_upload_params()
-    p.reserved[1] = 3
+    p.reserved = 3
     assert _abi.lib().sp_scene_upload_ex(scene.handle, 0, C.byref(p)) == _abi.SP_ERR_ARG
