@@ -20,6 +20,9 @@ hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
 hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream);
+bool       has_probe(int integ);
+hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
+                        hipStream_t stream);
 } // namespace spd
 
 namespace {
@@ -1256,10 +1259,12 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // ab_tile_order.txt): many tiles per persistent wave and a probe that costs little of the
         // frame -- bunny 1080p @ 256 spp (7.9 tiles per wave) +3-4 %, lucy +2 %, elf's 8-way
         // shard +3 %; spheres 1024^2 (4 tiles per wave) lost 1 % at 256 spp and 5 % at 64 spp.
-        // SP_TILE_HOIST=<factor> forces it (test hook; 0 = queue order).
+        // DirectLighting and IterativeRRNEE have probe kernels (sp_probe_*.hip); the other
+        // integrators render in queue order.  SP_TILE_HOIST=<factor> forces it (test hook; 0 =
+        // queue order).
         float hoist = (n_tiles >= 6 * (int64_t)waves && p->samples_per_pixel >= 128) ? 2.0f : 0.0f;
         if (const char* v = std::getenv("SP_TILE_HOIST")) hoist = (float)std::atof(v);
-        if (hoist > 0.0f && n_tiles > (int64_t)waves) {
+        if (hoist > 0.0f && n_tiles > (int64_t)waves && spd::has_probe(integ)) {
             if ((size_t)n_tiles > s->order_cap) {
                 if (s->d_tile_time) (void)hipFree(s->d_tile_time);
                 if (s->d_order) (void)hipFree(s->d_order);
@@ -1276,7 +1281,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             pr.tile_time = s->d_tile_time;
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
-            SP_HIP(spd::launch_render(s->dev, pr, integ, variant, blocks, lds_bytes, stream));
+            SP_HIP(spd::launch_probe(s->dev, pr, integ, variant, blocks, lds_bytes, stream));
             SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, s->d_order, stream));
             SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
             a.order = s->d_order;

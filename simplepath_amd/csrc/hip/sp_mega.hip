@@ -24,13 +24,30 @@ hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int
     return hipGetLastError();
 }
 
+// the probe kernel of an integrator's megakernel (tile order below); nullptr: none built
+static KernelFn select_probe(int integ, int variant)
+{
+    if (integ == SP_INTEGRATOR_DIRECT_LIGHTING) return probe_direct(variant);
+    if (integ == SP_INTEGRATOR_ITERATIVE_RRNEE) return probe_rrnee(variant);
+    return nullptr;
+}
+bool has_probe(int integ) { return select_probe(integ, 0) != nullptr; }
+hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
+                        hipStream_t stream)
+{
+    const KernelFn k = select_probe(integ, variant);
+    if (!k) return hipErrorInvalidDeviceFunction;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);
+    return hipGetLastError();
+}
+
 // Tile order for the persistent megakernel.  Each wave renders its tiles one after another, and a
 // tile's cost spans two orders of magnitude (bunny 1080p @ 256 spp: 1 ms of sky to 234 ms of
 // glossy floor under a bunny); in queue order the most expensive tiles can be taken late, and the
 // frame ends with a tail in which a few waves finish them alone (profiles/r03/tile_timeline_*:
 // the last 15 % of the span ran below full occupancy, 9 % of the frame).  A probe pass renders
-// one sample of every tile (sp_render_kernel with spp = 1 and tile_time set: the same code, its
-// radiance discarded; the render re-seeds every pixel's stream) and times each tile; this kernel
+// one sample of every tile (sp_probe_kernel with spp = 1: the render's code writing tile times
+// instead of radiance; the render re-seeds every pixel's stream) and times each tile; this kernel
 // then moves the tiles whose probe time exceeds `factor` x the mean to the front of the queue.
 // Both classes keep queue order among themselves (a stable partition), so the spatial coherence of
 // consecutive tiles -- which a full longest-first sort loses -- is kept for the rest.

@@ -24,8 +24,11 @@ __device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
 // pulls 8x8 tiles from the queue (TileScheduler::get_next_tile) and owns one MT state slot.
 // One instantiation per integrator so each carries only its own live state; MINW is the
 // __launch_bounds__ occupancy request (waves per SIMD) chosen by measurement.
-template <int INTEG, int MINW>
-__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(Scene sc, RenderArgs args)
+// PROBE: the tile-order probe pass (sp_mega.hip) -- the same code writing each tile's wave time
+// to args.tile_time instead of radiance, compiled as its own kernel (sp_probe_kernel) so that
+// profiles list the probe and the render apart.
+template <int INTEG, bool PROBE>
+__device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderArgs& args)
 {
     extern __shared__ uint32_t lds[];
     const int tid  = threadIdx.x;
@@ -54,7 +57,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         const int64_t item = __shfl(grabbed, 0, 64);
         if (item >= args.num_tiles) break;
         const int64_t  slot    = args.order ? args.order[item] : item;
-        const uint64_t t_start = (args.tile_diag || args.tile_time) ? __builtin_amdgcn_s_memrealtime() : 0;
+        const uint64_t t_start = (PROBE || args.tile_diag) ? __builtin_amdgcn_s_memrealtime() : 0;
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
         const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
         const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
@@ -95,7 +98,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
             samples_total += args.spp;
             draws_total += rng.draws;
         }
-        if (args.tile_time) { // probe pass (sp_mega.hip tile_order): how long this tile kept the wave
+        if constexpr (PROBE) { // probe pass (sp_mega.hip tile_order): how long this tile kept the wave
             if (lane == 0) args.tile_time[slot] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
             continue;
         }
@@ -127,6 +130,16 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(S
         if (lane == 0 && s) atomicAdd(args.counters + k, s);
     }
 }
+template <int INTEG, int MINW>
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_render_kernel(Scene sc, RenderArgs args)
+{
+    render_tiles_body<INTEG, false>(sc, args);
+}
+template <int INTEG, int MINW>
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_probe_kernel(Scene sc, RenderArgs args)
+{
+    render_tiles_body<INTEG, true>(sc, args);
+}
 
 using KernelFn = void (*)(Scene, RenderArgs);
 KernelFn mega_direct(int variant);
@@ -134,6 +147,8 @@ KernelFn mega_iterative(int integ);
 KernelFn mega_rrnee(int waves);
 KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
+KernelFn probe_direct(int variant); // nullptr: no probe kernel (queue order)
+KernelFn probe_rrnee(int waves);
 hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream);
 
 } // namespace spd

@@ -152,7 +152,8 @@ def test_tile_order_probe_is_invisible(scene_dir, monkeypatch, integrator):
     s = load(scene_dir, "bunny.sp", 640, 512)  # 5120 tiles: more than the persistent waves (4096)
     monkeypatch.setenv("SP_TILE_HOIST", "2")    # forced: AUTO uses it from 6 tiles per wave and 128 spp
     ref, rst = sp.render_tiles(s, integrator, 2, pipeline="megakernel")
-    assert rst.launches == 3  # probe, partition, render
+    # probe, partition, render; integrators without a probe kernel (sp_probe_*.hip) keep queue order
+    assert rst.launches == (1 if integrator == "whitted" else 3)
     monkeypatch.setenv("SP_TILE_HOIST", "0")
     off, ost = sp.render_tiles(s, integrator, 2, pipeline="megakernel")
     assert ost.launches == 1
