@@ -435,12 +435,18 @@ def roofline_of(stats, pixels, args, kernel_ms):
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "ck_camera+ck_count+ck_shade+ck_sum",
                 "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg,
                 "valu": valu_of(args, "ck_shade")}  # the shading kernel: most of the four kernels' time
-    if st.pipeline == 1 or args.integrator != "direct_lighting":  # megakernel, or the sp_wpath rounds
+    if st.pipeline == 1 or args.integrator != "direct_lighting":  # megakernel
+        # stage_ms[0]: the render kernel alone, [1]: the tile-order probe + partition before it
+        # (HIP events on the render stream; sp_render_stats)
+        render_ms = sum(s.stage_ms[0] for s in stats) / n
+        probe_ms = sum(s.stage_ms[1] for s in stats) / n
+        if not render_ms > 0:
+            render_ms, probe_ms = kernel_ms, 0.0
         alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES
-        achieved = alg / (kernel_ms * 1e-3) / 1e9
+        achieved = alg / (render_ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "sp_render_kernel",
-                "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg,
+                "kernel_ms": round(render_ms, 3), "probe_ms": round(probe_ms, 3), "alg_bytes_per_launch": alg,
                 "valu": valu_of(args, "sp_render_kernel")}
     names = ["wf_init+wf_resolve", "wf_primary", "wf_shade", "wf_shadow"]
     tot = [sum(s.stage_ms[k] for s in stats) / n for k in range(4)]

@@ -247,6 +247,7 @@ typedef struct sp_render_stats {
     uint64_t primary_hits;    /* wavefront: camera rays that hit geometry (shading work items)     */
     float    stage_ms[4];     /* with SP_RENDER_STAGE_TIMING, wavefront: [init+resolve, primary,   */
                               /* shade, shadow] of part 0 summed over launches; megakernel: [0]   */
+                              /* the render kernel, [1] the tile-order probe + partition           */
     int32_t  parts;           /* wavefront: concurrent parts (streams); part 0 holds ceil(tiles/2) */
     int32_t  stack_depth;     /* traversal-stack entries per lane the BVH walks needed (ABI 3)      */
 } sp_render_stats;
