@@ -606,6 +606,17 @@ float sp_host_rsqrt_emulated(float x)
     return spm::rsqrtss_emulated(x, t);
 }
 
+// Words of LDS traversal stack per lane.  The binary walks push at most one deferred child per
+// level; the wide walks one child group per level, and the closest-hit form keeps each group's
+// entry distance in the upper half.  Once closest hits walk the wide BVH (SAH scenes), no query
+// walks the binary geometry BVH, so its depth no longer sizes the stack -- only the wide and the
+// light BVH's do (lucy 30 -> 22 words: a fourth 4-wave block fits a CU's LDS).
+static int stack_entries(int depth, int wide_depth, int light_depth, bool wide_closest)
+{
+    if (wide_closest) return std::max(2 * (wide_depth + 1), light_depth + 1);
+    return std::max(depth, std::max(wide_depth, light_depth)) + 1;
+}
+
 static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params* up_params)
 {
     if (!s) return fail(SP_ERR_ARG, "null scene");
@@ -831,8 +842,7 @@ static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params
     // distance per entry in the upper half.
     d.ordered     = bvh_mode == 1 ? 0 : 1; // reference order is part of the bit-exact contract
     d.wide_closest = (opts.wide_closest && !wide.words.empty()) ? 1 : 0;
-    d.stack_depth  = std::max(bvh.max_depth, std::max(wide.depth, lbvh.max_depth)) + 1;
-    if (d.wide_closest) d.stack_depth = std::max(d.stack_depth, 2 * (wide.depth + 1)); // + group distances
+    d.stack_depth  = stack_entries(bvh.max_depth, wide.depth, lbvh.max_depth, d.wide_closest != 0);
     d.stackless   = stackless ? 1 : 0;
     d.parents       = nullptr;
     d.light_parents = nullptr;
@@ -1432,8 +1442,8 @@ int sp_scene_bvh_build_info(const sp_scene* s, int32_t bvh_mode, sp_bvh_info* ou
         out->light_depth           = light_bvh(h, lids, lpart).max_depth;
         const bool stackless       = stackless_for(opts, std::max(out->depth, out->light_depth));
         if (wide_enabled(opts) && !bvh.nodes.empty() && !stackless) out->wide_depth = sph::build_wide(bvh).depth;
-        out->stack_depth = stackless ? 0 : std::max(out->depth, std::max(out->wide_depth, out->light_depth)) + 1;
-        if (out->wide_depth && opts.wide_closest) out->stack_depth = std::max(out->stack_depth, 2 * (out->wide_depth + 1));
+        out->stack_depth = stackless ? 0 : stack_entries(out->depth, out->wide_depth, out->light_depth,
+                                                          out->wide_depth && opts.wide_closest);
         return SP_OK;
     } catch (const std::exception& e) {
         return fail(SP_ERR_UNSUPPORTED, std::string("BVH build failed: ") + e.what());

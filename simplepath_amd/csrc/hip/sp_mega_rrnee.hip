@@ -1,4 +1,8 @@
 // sp_mega_rrnee.hip -- IterativeIntegratorRRNEE megakernel (lock-step samples, one lane per pixel).
+// Multiple-importance estimates served across the wave (sp_path.hpp serve_rho).
+#ifndef SP_SERVE_RHO
+#define SP_SERVE_RHO 1
+#endif
 #include "sp_mega.hpp"
 
 namespace spd {

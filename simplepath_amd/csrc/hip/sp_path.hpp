@@ -86,6 +86,14 @@ struct Rng {
     int       lin = 0, pre = 0;
     int       pfn = 0;        // valid words in pf (words idx .. idx + pfn - 1 of buffer cur)
     uint64_t  pf[RNG_PF > 0 ? RNG_PF : 1];
+#if SP_SERVE_RHO
+    // Wave-served selection weights (serve_rho): the estimates of this lane's next eval / pdf /
+    // sample call sites were computed by the wave at stream positions srv_pos, + srv_dc and
+    // + 2 srv_dc + srv_coat (draw counts); glossy_weights takes them from srv_w when the stream is
+    // exactly there.
+    bool      srv_on  = false;
+    uint32_t  srv_pos = 0, srv_dc = 0, srv_coat = 0;
+#endif
 };
 
 __device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_N * 64; }
@@ -246,6 +254,22 @@ __device__ __forceinline__ void rng_skip(Rng& r, int n)
         r.draws += (uint32_t)take;
         n -= take;
     }
+    r.pfn = 0;
+}
+
+// rng_skip for n words that rng_reserve(n) has made twist-free (n <= MT_N): the same state,
+// without inlining a twist at the call site.
+__device__ __forceinline__ void rng_skip_reserved(Rng& r, int n)
+{
+    const int t = r.idx + n;
+    if (t > MT_N) {
+        r.cur   = mt_next(r);
+        r.idx   = t - MT_N;
+        r.ready = r.pre;
+    } else {
+        r.idx = t;
+    }
+    r.draws += (uint32_t)n;
     r.pfn = 0;
 }
 
@@ -1582,9 +1606,30 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
     return cdivs(r, (float)16u);
 }
 
+#if SP_SERVE_RHO
+// [wave][call site k][weight][owner lane]: weights served to the owners (serve_rho)
+static __shared__ float   srv_w[4][3][2][64];
+static __shared__ uint8_t srv_req[4][3 * 64]; // request r: owner lane | k << 6
+#endif
+
 // OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
 __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
 {
+#if SP_SERVE_RHO
+    if (rng.srv_on) {
+        // the same estimate (same material, wo and stream words) was computed by the wave: take it
+        // and advance the stream past its words
+        const uint32_t d = rng.draws - rng.srv_pos;
+        const int      k = (d == 0u) ? 0 : (d == rng.srv_dc) ? 1 : (d == 2u * rng.srv_dc + rng.srv_coat) ? 2 : -1;
+        if (k >= 0) {
+            const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            w[0]           = srv_w[wave][k][0][lane];
+            w[1]           = srv_w[wave][k][1][lane];
+            rng_skip_reserved(rng, (int)rng.srv_dc);
+            return;
+        }
+    }
+#endif
     rgb r0;
     SP_WPROF(1, r0 = mf_rho16(m, wo, rng, q));
     const rgb r1 = cscale(m.lambert_albedo, k_pi); // LambertianBRDF::rho_impl
@@ -2100,13 +2145,18 @@ __device__ __forceinline__ rgb integrate_whitted(Ctx& c, Ray ray)
     return acc;
 }
 
-// estimate_direct_mis (Integrators/Integrator.cpp:486)
-__device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p, f3 n, f3 wo, int mid)
+// estimate_direct_mis (Integrators/Integrator.cpp:486), in two parts: the light sample and its
+// shadow ray (true: the light sample is usable and unoccluded), then the rest
+__device__ __forceinline__ bool mis_light_part(Ctx& c, const Light& l, f3 p, f3 n, LSample& ls)
 {
-    rgb           Lr = mkc(0, 0, 0);
-    const LSample ls = light_sample(c.sc, l, p, n, next2D(c.rng), c.q);
-    if (ls.pdf == 0.0f || cblack(ls.L)) return Lr;
-    if (occluded(c, ls.ray, ls.tmin, ls.tmax)) return Lr;
+    ls = light_sample(c.sc, l, p, n, next2D(c.rng), c.q);
+    if (ls.pdf == 0.0f || cblack(ls.L)) return false;
+    if (occluded(c, ls.ray, ls.tmin, ls.tmax)) return false;
+    return true;
+}
+__device__ __forceinline__ rgb mis_material_part(Ctx& c, const Light& l, const LSample& ls, f3 p, f3 n, f3 wo, int mid)
+{
+    rgb       Lr = mkc(0, 0, 0);
     const f3  wi = ls.ray.d;
     const rgb be = material_eval(c.sc, mid, wo, wi, n, c.rng, c.q);
     if (!cblack(be)) {
@@ -2134,7 +2184,164 @@ __device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p,
     }
     return Lr;
 }
+__device__ __forceinline__ rgb estimate_direct_mis(Ctx& c, const Light& l, f3 p, f3 n, f3 wo, int mid)
+{
+    LSample ls;
+    if (!mis_light_part(c, l, p, n, ls)) return mkc(0, 0, 0);
+    return mis_material_part(c, l, ls, p, n, wo, mid);
+}
 
+#if SP_SERVE_RHO
+// Wave-served selection-weight estimates (IterativeRRNEE).  After its shadow ray, a lane whose
+// light sample is usable and unoccluded runs the glossy 16-sample estimate at three call sites
+// in a row -- Material::eval, Material::pdf, Material::sample (Integrator.cpp:505-519) -- all with
+// the same material and wo, at stream positions that are known in advance: eval's estimate takes
+// the next 32 words (none when wo.y == 0), pdf's the 32 after them, and sample's starts one word
+// later for a clearcoat (its Fresnel draw).  In lock step each call site costs the wave a full
+// estimate however few lanes reach it.  Here the wave lists every such lane's three estimates,
+// deals them out to all 64 lanes (dead paths and occluded lanes included), and each lane computes
+// the estimates it is dealt from the owner's own stream words, read where the owner's state lives
+// (the owner reserved the next generation first, so no twist happens in between).  The owners
+// then take the weights at their call sites (glossy_weights) and skip the words.  Every estimate
+// is the same function of the same inputs, so images, ray and draw counts are bit-identical.
+// The sample call site's estimate is speculative: it is unused if the coat draw picks the
+// specular lobe, and if eval's result is black (pdf's estimate then does not run) its position
+// does not match and the owner computes it itself.
+// One served estimate: glossy_weights at word idx of generation buffer cur of the owner's stream
+// (reserved by the owner).  Inlined: 744-747 against 736-743 Mrays/s as a called function (elf
+// 1024^2 @ 16 spp, profiles/r03/ab_rrnee_served.txt).
+__device__ __forceinline__ void served_weights(const Material& m, f3 wo, uint64_t* base, int cur, int idx, const Rsq& q,
+                                               float w[2])
+{
+    Rng sr;
+    sr.base  = base;
+    sr.cur   = cur;
+    sr.idx   = idx;
+    sr.ready = 1;
+    sr.draws = 0;
+    glossy_weights(m, wo, sr, q, w);
+}
+__device__ __forceinline__ void serve_rho(Ctx& c, bool want, int mid, f3 n, f3 wo)
+{
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    f3        wl   = mk(0, 0, 0);
+    int       base = 0;
+    uint32_t  dc = 0, coat = 0, pw = 0;
+    if (want) {
+        const Material& mm = c.sc.materials[mid];
+        coat               = (mm.kind == SP_MAT_CLEARCOAT) ? 1u : 0u;
+        base               = coat ? mm.base : mid;
+        wl                 = to_onb(onb_from_v(n, c.q), wo); // the wo every call site passes on
+        dc                 = (wl.y == 0.0f) ? 0u : 32u;      // mf_sample draws nothing when wo.y == 0
+        rng_reserve(c.rng, (int)(3u * dc + coat));
+        pw = ((uint32_t)c.rng.cur << 16) | (uint32_t)c.rng.idx;
+        const int first = 3 * __popcll(m & ((1ull << lane) - 1ull));
+        for (int k = 0; k < 3; ++k) srv_req[wave][first + k] = (uint8_t)(lane | (k << 6));
+        c.rng.srv_on   = true;
+        c.rng.srv_pos  = c.rng.draws;
+        c.rng.srv_dc   = dc;
+        c.rng.srv_coat = coat;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int total = 3 * __popcll(m);
+    for (int r0 = 0; r0 < total; r0 += 64) {
+        const int      r = r0 + lane;
+        const uint32_t e = (r < total) ? (uint32_t)srv_req[wave][r] : 0u;
+        const int      o = (int)(e & 63u), k = (int)(e >> 6);
+        // the owner's inputs (all lanes take part in the exchange)
+        const f3       owo   = mk(__shfl(wl.x, o, 64), __shfl(wl.y, o, 64), __shfl(wl.z, o, 64));
+        const int      obase = __shfl(base, o, 64);
+        const uint32_t opw   = (uint32_t)__shfl((int)pw, o, 64);
+        const uint32_t odc   = (uint32_t)__shfl((int)dc, o, 64);
+        const uint32_t ocoat = (uint32_t)__shfl((int)coat, o, 64);
+        if (r < total) {
+            int cur = (int)(opw >> 16);
+            int idx = (int)(opw & 0xffffu) + (int)(k == 0 ? 0u : k == 1 ? odc : 2u * odc + ocoat);
+            if (idx >= MT_N) {
+                cur ^= 1; // the megakernel's two-generation ring
+                idx -= MT_N;
+            }
+            float w[2];
+            served_weights(c.sc.materials[obase], owo, c.rng.base - lane + o, cur, idx, c.q, w);
+            srv_w[wave][k][0][o] = w[0];
+            srv_w[wave][k][1][o] = w[1];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// IntegratorIterativeRRNEE (Integrators/Integrator.cpp:550) with wave-served estimates: the same
+// per-lane operations as the form below, but a lane whose path has ended stays in the loop (no
+// break) so that every lane of the wave is there to serve estimates.
+__device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
+{
+    rgb   throughput = mkc(1, 1, 1);
+    rgb   L          = mkc(0, 0, 0);
+    float tmin = k_ray_epsilon, tmax = k_infinite;
+    constexpr float rr_cut = 0.1f;
+    bool  alive = true;
+    for (int depth = 0; depth < c.sc.max_depth; ++depth) {
+        if (!__any(alive)) break;
+        Query   qr;
+        MSample s;
+        f3      wo  = mk(0, 0, 0), n = mk(0, 0, 0);
+        bool    hit = false;
+        if (alive) {
+            rng_prepare(c.rng);
+            qr = trace(c, ray, tmin, tmax);
+            if (qr.geom) {
+                wo = neg(ray.d);
+                n  = qr.is.n;
+                s  = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
+                if (s.pdf == 0.0f || cblack(s.color)) alive = false;
+                else hit = true;
+            } else {
+                if (qr.lh.hit) L = cadd(L, cmul(throughput, light_hit_L(c.sc, qr.lh, ray.d, c.q)));
+                alive = false;
+            }
+        }
+        for (int li = 0; li < c.sc.n_lights; ++li) {
+            LSample ls;
+            bool    go = false, want = false;
+            if (hit) {
+                go   = mis_light_part(c, c.sc.lights[li], qr.is.p, n, ls);
+                want = go && material_has_rho(c.sc, qr.is.material);
+            }
+            serve_rho(c, want, want ? qr.is.material : 0, n, wo);
+            if (hit) {
+                const rgb e    = go ? mis_material_part(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material) : mkc(0, 0, 0);
+                c.rng.srv_on   = false;
+                L              = cadd(L, cmul(throughput, e));
+            }
+        }
+        if (hit) {
+            const f3    next_o = ray_at(ray, qr.is.t);
+            const f3    wi     = s.dir;
+            const float cosine = abs_f(dot(wi, n));
+            throughput         = cmul(throughput, cdivs(cscale(s.color, cosine), s.pdf));
+            if (depth >= c.sc.rr_depth) {
+                const float lum = luminance(throughput);
+                if (lum < rr_cut) {
+                    const float qv = std_max(0.05f, lum / rr_cut);
+                    if (next1D(c.rng) < qv) throughput = cdivs(throughput, qv);
+                    else alive = false;
+                }
+            }
+            ray.o = next_o;
+            ray.d = wi;
+            tmin  = ray_offset(cosine);
+            tmax  = k_infinite;
+        }
+    }
+    return L;
+}
+#else
 // IntegratorIterativeRRNEE (Integrators/Integrator.cpp:550)
 __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
 {
@@ -2177,6 +2384,7 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
     }
     return L;
 }
+#endif
 
 // ============================================================================ the kernel
 // MandelbrotIntegrator::integrate_impl + mandel (Integrators/Integrator.cpp:59-105) with

@@ -82,6 +82,15 @@ def full_scene(name):
     return _scenes[name]
 
 
+def expected_stack(built, bvh):
+    # LDS stack words the render uses: the goldens recorded the host build's depths; on the SAH BVH
+    # closest hits walk the 8-wide BVH, so the wide depth (one group + its distance per level) and
+    # the light BVH size the stack, not the binary depth (sp_capi.hip stack_entries)
+    if bvh == 0 and built["wide_depth"] > 0:
+        return max(2 * (built["wide_depth"] + 1), built["light_depth"] + 1)
+    return built["stack_depth"]
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name", ["elf", "lucy"])
 @pytest.mark.parametrize("bvh", [1, 0])
@@ -94,7 +103,7 @@ def test_full_scale_tiles_vs_reference(name, bvh):
     ids = g["tile_ids"].astype(np.int32)
     ref = g["radiance"]
     out, st = sp.render_tiles(s, int(g["integrator"]), int(g["spp"]), ids)
-    assert st.stack_depth == built["stack_depth"]
+    assert st.stack_depth == expected_stack(built, bvh)
     assert st.samples > 0 and st.rays > st.samples
     r = rel_l2(out, ref)
     frac = float(np.mean(np.all(out == ref, axis=-1)))
@@ -159,7 +168,7 @@ def test_full_scale_lucy_sah_megakernel():
     out, st = sp.render_tiles(s, "direct_lighting", int(g["spp"]), ids, pipeline="megakernel")
     assert st.pipeline == sp.PIPELINES["megakernel"]
     built = json.loads(str(g["bvh_sah"]))
-    assert st.stack_depth == built["stack_depth"]
+    assert st.stack_depth == expected_stack(built, 0)
     r = rel_l2(out, ref)
     frac = float(np.mean(np.all(out == ref, axis=-1)))
     print(f"lucy SAH megakernel: rel_l2={r:.3e}, bit-exact pixels {frac:.5f}")
