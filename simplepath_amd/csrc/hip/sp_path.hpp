@@ -305,8 +305,9 @@ __device__ __forceinline__ void rng_reserve(Rng& r, int n)
 
 // SP_RHO_TOUCH: the 16-sample glossy estimate touches its 32 words first; the DMA target is one
 // 256-byte LDS sink per block.  Per translation unit: on in the DirectLighting megakernel (with
-// no draw-ahead window: bunny 2720 -> 2762 Mrays/s), off elsewhere (elf's IterativeRRNEE
-// megakernel 553 -> 541, the 8-way chunk shard unchanged; profiles/r02/s5).
+// no draw-ahead window: bunny 2720 -> 2762 Mrays/s, profiles/r02/s5), the sample chunks (round 2
+// session 6) and the IterativeRRNEE megakernel once its estimates are served across the wave
+// (739-745 -> 746-757 on elf; the lock-step kernel had lost with it, 553 -> 541).
 #ifndef SP_RHO_TOUCH
 #define SP_RHO_TOUCH 0
 #endif

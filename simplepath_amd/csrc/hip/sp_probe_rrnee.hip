@@ -1,9 +1,13 @@
 // sp_probe_rrnee.hip -- tile-order probe kernels of the IterativeRRNEE megakernel (sp_mega.hpp
 // sp_probe_kernel, same settings as sp_mega_rrnee.hip).
-// Multiple-importance estimates served across the wave (sp_path.hpp serve_rho).
+// Multiple-importance estimates served across the wave (sp_path.hpp serve_rho).  With them, no
+// RNG draw-ahead window and the estimate's words touched in advance (as in the DirectLighting
+// megakernel): elf 1024^2 @ 16 spp 739-745 -> 746-757 Mrays/s (profiles/r03/ab_rrnee_served.txt).
 #ifndef SP_SERVE_RHO
 #define SP_SERVE_RHO 1
 #endif
+#define SP_RNG_PF 0
+#define SP_RHO_TOUCH 1
 #include "sp_mega.hpp"
 
 namespace spd {
