@@ -66,6 +66,30 @@ __device__ __forceinline__ float rsqrt_ref(float a, const Rsq& q)
 }
 __device__ __forceinline__ f3 normalize(f3 a, const Rsq& q) { return scale(a, rsqrt_ref(dot(a, a), q)); }
 
+// Correctly rounded sqrt of max(0, 1 - v * v)-shaped arguments: x is +0 or at least 2^-24 (1 - v^2
+// below 1 is exact near 1 and at least 1 - (1 - 2^-24)), never denormal, negative or inf.  This is
+// the compiler's own exact f32 sqrt (v_sqrt_f32 and a one-ulp correction from two FMA residuals)
+// without the two parts such x never reach: scaling inputs below 2^-96, and passing 0 / inf
+// through (for +0 the correction already returns +0).  16 -> 9 instructions, same bits.
+#ifndef SP_SQRT_UNIT
+#define SP_SQRT_UNIT 1
+#endif
+__device__ __forceinline__ float sqrt_unit(float x)
+{
+#if SP_SQRT_UNIT
+    const float s  = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+    const float su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float vp = __builtin_fmaf(-sd, s, x);
+    const float vs = __builtin_fmaf(-su, s, x);
+    float       r  = (vp <= 0.0f) ? sd : s;
+    r              = (vs > 0.0f) ? su : r;
+    return r;
+#else
+    return sqrt_f(x);
+#endif
+}
+
 // Draw-ahead window: the next RNG_PF words of the current generation are loaded RNG_PF draws
 // before they are consumed, so a draw does not wait for a global load (the state lives in HBM,
 // 160 KB per wave).  The window never crosses into the other buffer and is emptied at every
@@ -1208,7 +1232,7 @@ __device__ __forceinline__ bool scene_any(const Scene& sc, const Ray& ray, float
 __device__ __forceinline__ f3 sample_uniform_sphere(P2 u)
 {
     const float z   = 1.0f - 2.0f * u.x;
-    const float r   = sqrt_f(std_max(0.0f, 1.0f - z * z));
+    const float r   = sqrt_unit(std_max(0.0f, 1.0f - z * z));
     const float phi = (float)(2.0 * (double)k_pi * (double)u.y);
     return mk(r * lm_cosf<true>(phi), r * lm_sinf<true>(phi), z); // u in [0, 1): |phi| < 2 pi
 }
@@ -1216,7 +1240,7 @@ __device__ __forceinline__ f3 sample_uniform_sphere(P2 u)
 __device__ __forceinline__ f3 sample_uniform_hemisphere(P2 u)
 {
     const float y   = u.x;
-    const float r   = sqrt_f(std_max(0.0f, 1.0f - y * y));
+    const float r   = sqrt_unit(std_max(0.0f, 1.0f - y * y));
     const float phi = 2.0f * k_pi * u.y;
     return mk(r * lm_cosf<true>(phi), y, r * lm_sinf<true>(phi)); // u in [0, 1): |phi| < 2 pi
 }
@@ -1239,7 +1263,7 @@ __device__ __forceinline__ P2 concentric_disk(P2 u)
 __device__ __forceinline__ f3 sample_cosine_hemisphere(P2 u)
 {
     const P2    d = concentric_disk(u);
-    const float y = sqrt_f(std_max(0.0f, 1.0f - d.x * d.x - d.y * d.y));
+    const float y = sqrt_unit(std_max(0.0f, 1.0f - d.x * d.x - d.y * d.y)); // 0 or >= 2^-48
     return mk(d.x, y, d.y);
 }
 constexpr float k_uniform_sphere_pdf     = 1.0f / (4.0f * k_pi);
@@ -1277,7 +1301,7 @@ constexpr int PROP_DIFFUSE = 1, PROP_GLOSSY = 2, PROP_SPECULAR = 4, PROP_REFLECT
 
 __device__ __forceinline__ float cos2_theta(f3 w) { return w.y * w.y; }
 __device__ __forceinline__ float sin2_theta(f3 w) { return std_max(0.0f, 1.0f - cos2_theta(w)); }
-__device__ __forceinline__ float sin_theta(f3 w) { return sqrt_f(sin2_theta(w)); }
+__device__ __forceinline__ float sin_theta(f3 w) { return sqrt_unit(sin2_theta(w)); }
 __device__ __forceinline__ float tan_theta(f3 w) { return sin_theta(w) / w.y; }
 __device__ __forceinline__ float tan2_theta(f3 w) { return sin2_theta(w) / cos2_theta(w); }
 __device__ __forceinline__ float cos_phi(f3 w)
@@ -1300,10 +1324,10 @@ __device__ __forceinline__ float fresnel_dielectric(float cos_i, float eta_i, fl
         const float s = eta_i; eta_i = eta_t; eta_t = s;
         cos_i = abs_f(cos_i);
     }
-    const float sin_i = sqrt_f(std_max(0.0f, 1.0f - cos_i * cos_i));
+    const float sin_i = sqrt_unit(std_max(0.0f, 1.0f - cos_i * cos_i));
     const float sin_t = eta_i / eta_t * sin_i;
     if (sin_t >= 1) return 1.0f;
-    const float cos_t = sqrt_f(std_max(0.0f, 1.0f - sin_t * sin_t));
+    const float cos_t = sqrt_unit(std_max(0.0f, 1.0f - sin_t * sin_t));
     const float parl  = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
     const float perp  = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
     return (parl * parl + perp * perp) / 2.0f;
@@ -1351,7 +1375,7 @@ __device__ __forceinline__ P2 beckmann_sample11(float cos_theta_i, float U1, flo
         s.y = r * sp;
         return s;
     }
-    const float sin_theta_i = sqrt_f(std_max(0.0f, 1.0f - cos_theta_i * cos_theta_i));
+    const float sin_theta_i = sqrt_unit(std_max(0.0f, 1.0f - cos_theta_i * cos_theta_i));
     const float tan_theta_i = sin_theta_i / cos_theta_i;
     const float cot_theta_i = 1.0f / tan_theta_i;
     float       a           = -1.0f;
@@ -1492,7 +1516,7 @@ __device__ __forceinline__ BeckPre beck_pre(const Material& m, f3 wo, const Rsq&
     p.steep              = cos_t > .9999f;
     p.tan_theta_i = p.c0 = p.fit = p.normalization = p.sqrt_pi_inv = 0.0f;
     if (!p.steep) {
-        const float sin_theta_i = sqrt_f(std_max(0.0f, 1.0f - cos_t * cos_t));
+        const float sin_theta_i = sqrt_unit(std_max(0.0f, 1.0f - cos_t * cos_t));
         p.tan_theta_i           = sin_theta_i / cos_t;
         const float cot_theta_i = 1.0f / p.tan_theta_i;
         p.c0                    = lm_erff(cot_theta_i);
@@ -1859,7 +1883,7 @@ __device__ __forceinline__ float sphere_pdf(const Light& l, f3 observer_world)
     if (sqr <= 1.0f) return k_uniform_sphere_pdf;
     constexpr float sin2_1_5_deg = 0.00068523f;
     const float     sin2_max     = 1.0f / sqr;
-    const float     cos_max      = sqrt_f(std_max(0.0f, 1.0f - sin2_max));
+    const float     cos_max      = sqrt_unit(std_max(0.0f, 1.0f - sin2_max));
     const float     omc          = (sin2_max < sin2_1_5_deg) ? sin2_max / 2.0f : 1.0f - cos_max;
     return 1.0f / (2.0f * k_pi * omc);
 }
