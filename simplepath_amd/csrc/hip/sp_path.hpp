@@ -115,8 +115,12 @@ struct Rng {
     // sample call sites were computed by the wave at stream positions srv_pos, + srv_dc and
     // + 2 srv_dc + srv_coat (draw counts); glossy_weights takes them from srv_w when the stream is
     // exactly there.
-    bool      srv_on  = false;
-    uint32_t  srv_pos = 0, srv_dc = 0, srv_coat = 0;
+    // srv_on: 0 off; 1 served weights available (srv_B: eval / pdf / sample of the light being
+    // estimated, srv_A: the bounce's own Material::sample at srv_posA); 2 defer the bounce's
+    // Material::sample estimate (glossy_weights records where it starts and skips its words).
+    int       srv_on  = 0;
+    bool      srv_A = false, srv_B = false;
+    uint32_t  srv_pos = 0, srv_dc = 0, srv_coat = 0, srv_posA = 0, srv_pwA = 0;
 #endif
 };
 
@@ -1633,19 +1637,35 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
 
 #if SP_SERVE_RHO
 // [wave][call site k][weight][owner lane]: weights served to the owners (serve_rho)
-static __shared__ float   srv_w[4][3][2][64];
-static __shared__ uint8_t srv_req[4][3 * 64]; // request r: owner lane | k << 6
+static __shared__ float   srv_w[4][4][2][64];
+static __shared__ uint8_t srv_req[4][4 * 64]; // request r: owner lane | k << 6 (k = 3: the bounce's sample)
 #endif
 
 // OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
 __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
 {
 #if SP_SERVE_RHO
-    if (rng.srv_on) {
+    if (rng.srv_on == 2) {
+        // the bounce's Material::sample, deferred (integrate_rrnee): note where its estimate starts
+        // and skip the words; the weights {0, 1} pick the lambertian lobe, which draws the same
+        // three words after the estimate as either lobe can with the real weights (the glossy one
+        // draws none only when wo.y == 0, and then its weight is 0)
+        rng.srv_A    = true;
+        rng.srv_dc   = wo.y == 0.0f ? 0u : 32u;
+        rng.srv_posA = rng.draws;
+        rng.srv_pwA  = ((uint32_t)rng.cur << 16) | (uint32_t)rng.idx;
+        w[0]         = 0.0f;
+        w[1]         = 1.0f;
+        rng_skip_reserved(rng, (int)rng.srv_dc);
+        return;
+    }
+    if (rng.srv_on == 1) {
         // the same estimate (same material, wo and stream words) was computed by the wave: take it
         // and advance the stream past its words
         const uint32_t d = rng.draws - rng.srv_pos;
-        const int      k = (d == 0u) ? 0 : (d == rng.srv_dc) ? 1 : (d == 2u * rng.srv_dc + rng.srv_coat) ? 2 : -1;
+        int            k = -1;
+        if (rng.srv_A && rng.draws == rng.srv_posA) k = 3;
+        else if (rng.srv_B) k = (d == 0u) ? 0 : (d == rng.srv_dc) ? 1 : (d == 2u * rng.srv_dc + rng.srv_coat) ? 2 : -1;
         if (k >= 0) {
             const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
             w[0]           = srv_w[wave][k][0][lane];
@@ -2246,33 +2266,43 @@ __device__ __forceinline__ void served_weights(const Material& m, f3 wo, uint64_
     sr.draws = 0;
     glossy_weights(m, wo, sr, q, w);
 }
-__device__ __forceinline__ void serve_rho(Ctx& c, bool want, int mid, f3 n, f3 wo)
+// want: this lane's eval / pdf / sample estimates of the light being estimated (k = 0, 1, 2);
+// want_a: its deferred Material::sample of the bounce (k = 3, at c.rng.srv_pwA).  All lanes call.
+__device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mid, f3 n, f3 wo)
 {
-    const uint64_t m = __ballot(want);
-    if (m == 0) return;
+    const uint64_t mb = __ballot(want), ma = __ballot(want_a);
+    if ((mb | ma) == 0) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     f3        wl   = mk(0, 0, 0);
     int       base = 0;
-    uint32_t  dc = 0, coat = 0, pw = 0;
-    if (want) {
+    uint32_t  dc = 0, coat = 0, pw = 0, pwa = 0;
+    if (want || want_a) {
         const Material& mm = c.sc.materials[mid];
         coat               = (mm.kind == SP_MAT_CLEARCOAT) ? 1u : 0u;
         base               = coat ? mm.base : mid;
         wl                 = to_onb(onb_from_v(n, c.q), wo); // the wo every call site passes on
         dc                 = (wl.y == 0.0f) ? 0u : 32u;      // mf_sample draws nothing when wo.y == 0
-        rng_reserve(c.rng, (int)(3u * dc + coat));
-        pw = ((uint32_t)c.rng.cur << 16) | (uint32_t)c.rng.idx;
-        const int first = 3 * __popcll(m & ((1ull << lane) - 1ull));
-        for (int k = 0; k < 3; ++k) srv_req[wave][first + k] = (uint8_t)(lane | (k << 6));
-        c.rng.srv_on   = true;
-        c.rng.srv_pos  = c.rng.draws;
-        c.rng.srv_dc   = dc;
-        c.rng.srv_coat = coat;
+        const uint64_t lt  = (1ull << lane) - 1ull;
+        int            r   = 3 * __popcll(mb & lt) + __popcll(ma & lt);
+        if (want) {
+            rng_reserve(c.rng, (int)(3u * dc + coat));
+            pw = ((uint32_t)c.rng.cur << 16) | (uint32_t)c.rng.idx;
+            for (int k = 0; k < 3; ++k) srv_req[wave][r++] = (uint8_t)(lane | (k << 6));
+            c.rng.srv_on   = 1;
+            c.rng.srv_B    = true;
+            c.rng.srv_pos  = c.rng.draws;
+            c.rng.srv_dc   = dc;
+            c.rng.srv_coat = coat;
+        }
+        if (want_a) {
+            pwa                 = c.rng.srv_pwA;
+            srv_req[wave][r++] = (uint8_t)(lane | (3 << 6));
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int total = 3 * __popcll(m);
+    const int total = 3 * __popcll(mb) + __popcll(ma);
     for (int r0 = 0; r0 < total; r0 += 64) {
         const int      r = r0 + lane;
         const uint32_t e = (r < total) ? (uint32_t)srv_req[wave][r] : 0u;
@@ -2280,12 +2310,14 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, int mid, f3 n, f3 w
         // the owner's inputs (all lanes take part in the exchange)
         const f3       owo   = mk(__shfl(wl.x, o, 64), __shfl(wl.y, o, 64), __shfl(wl.z, o, 64));
         const int      obase = __shfl(base, o, 64);
-        const uint32_t opw   = (uint32_t)__shfl((int)pw, o, 64);
+        const uint32_t opb   = (uint32_t)__shfl((int)pw, o, 64);
+        const uint32_t opa   = (uint32_t)__shfl((int)pwa, o, 64);
+        const uint32_t opw   = (k == 3) ? opa : opb;
         const uint32_t odc   = (uint32_t)__shfl((int)dc, o, 64);
         const uint32_t ocoat = (uint32_t)__shfl((int)coat, o, 64);
         if (r < total) {
             int cur = (int)(opw >> 16);
-            int idx = (int)(opw & 0xffffu) + (int)(k == 0 ? 0u : k == 1 ? odc : 2u * odc + ocoat);
+            int idx = (int)(opw & 0xffffu) + (int)(k == 0 || k == 3 ? 0u : k == 1 ? odc : 2u * odc + ocoat);
             if (idx >= MT_N) {
                 cur ^= 1; // the megakernel's two-generation ring
                 idx -= MT_N;
@@ -2316,15 +2348,37 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
         Query   qr;
         MSample s;
         f3      wo  = mk(0, 0, 0), n = mk(0, 0, 0);
-        bool    hit = false;
+        bool    hit = false, pend = false;
+        Rng     snap = c.rng;
         if (alive) {
             rng_prepare(c.rng);
             qr = trace(c, ray, tmin, tmax);
             if (qr.geom) {
                 wo = neg(ray.d);
                 n  = qr.is.n;
-                s  = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
-                if (s.pdf == 0.0f || cblack(s.color)) alive = false;
+#if SP_SERVE_SAMPLE
+                // The bounce's Material::sample estimate joins the first light's served estimates:
+                // its words are skipped now (placeholder weights, the same draw count) and the call
+                // is repeated from here with the served weights after the first light's shadow ray.
+                // The whole bounce (at most 1 + 32 + 3 + 2 + 97 words up to that light's sample
+                // estimate) is reserved first, so none of these words is twisted over meanwhile.
+                const bool defer = c.sc.n_lights > 0;
+                if (defer) {
+                    rng_reserve(c.rng, 140);
+                    snap         = c.rng;
+                    c.rng.srv_on = 2;
+                    c.rng.srv_A  = false;
+                }
+#endif
+                s = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
+#if SP_SERVE_SAMPLE
+                if (defer) {
+                    pend         = c.rng.srv_A; // the estimate was reached (a glossy base, no specular coat pick)
+                    c.rng.srv_on = 0;
+                }
+#endif
+                if (pend) hit = true; // whether the sample is usable is known once it is finished
+                else if (s.pdf == 0.0f || cblack(s.color)) alive = false;
                 else hit = true;
             } else {
                 if (qr.lh.hit) L = cadd(L, cmul(throughput, light_hit_L(c.sc, qr.lh, ray.d, c.q)));
@@ -2332,16 +2386,41 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
             }
         }
         for (int li = 0; li < c.sc.n_lights; ++li) {
-            LSample ls;
-            bool    go = false, want = false;
+            LSample        ls;
+            bool           go = false, want = false;
+            const uint32_t rays0 = c.rays, shadow0 = c.shadow;
             if (hit) {
                 go   = mis_light_part(c, c.sc.lights[li], qr.is.p, n, ls);
                 want = go && material_has_rho(c.sc, qr.is.material);
             }
-            serve_rho(c, want, want ? qr.is.material : 0, n, wo);
+            serve_rho(c, want, li == 0 && pend, (want || pend) ? qr.is.material : 0, n, wo);
+#if SP_SERVE_SAMPLE
+            if (li == 0 && pend) {
+                // the deferred Material::sample, from the bounce's stream position, now with its weights
+                Rng ra      = snap;
+                ra.srv_on   = 1;
+                ra.srv_A    = true;
+                ra.srv_B    = false;
+                ra.srv_posA = c.rng.srv_posA;
+                ra.srv_dc   = c.rng.srv_dc;
+                s           = material_sample(c.sc, qr.is.material, wo, n, ra, c.q);
+                c.rng.srv_A = false;
+                if (s.pdf == 0.0f || cblack(s.color)) {
+                    // not usable: the path ends right after the sample (Integrator.cpp:566), so the
+                    // light's sample and shadow ray never happened -- stream and counters go back
+                    ra.srv_on = 0;
+                    ra.srv_A  = false;
+                    c.rng     = ra;
+                    c.rays    = rays0;
+                    c.shadow  = shadow0;
+                    hit = go = alive = false;
+                }
+            }
+#endif
             if (hit) {
                 const rgb e    = go ? mis_material_part(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material) : mkc(0, 0, 0);
-                c.rng.srv_on   = false;
+                c.rng.srv_on   = 0;
+                c.rng.srv_B    = false;
                 L              = cadd(L, cmul(throughput, e));
             }
         }

@@ -8,6 +8,11 @@
 #endif
 #define SP_RNG_PF 0
 #define SP_RHO_TOUCH 1
+// The bounce's own Material::sample estimate joins the first light's served round (sp_path.hpp
+// integrate_rrnee): 768-775 -> 783-797 Mrays/s on elf 1024^2 @ 16 spp (profiles/r03/ab_rrnee_served.txt).
+#ifndef SP_SERVE_SAMPLE
+#define SP_SERVE_SAMPLE 1
+#endif
 #include "sp_mega.hpp"
 
 namespace spd {
