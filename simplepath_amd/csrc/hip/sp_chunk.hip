@@ -180,6 +180,37 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
         const size_t p  = (size_t)slot * 64 + lane;
         rng.base        = a.gens + (size_t)slot * a.gens_per_px * (MT_N * 64) + lane;
         if (px.inside) rng_seed(rng, ((px.x << 16u) | px.y) ^ 0xb0ae9d99u); // main.cpp:73
+        if (a.draws) {
+            // Counts known from the camera pass: the stream position before sample i is the sum
+            // of the earlier counts, so the counts are summed in batches of loads that are all in
+            // flight together (not one dependent load per sample), and the generations are twisted
+            // after, one after the other -- the same positions (in the lazy-switch form rng_skip
+            // leaves: T > 0 draws -> generation ceil(T / 312), word T - 312 (generation - 1)) and
+            // the same generations as skipping sample by sample.
+            const uint16_t* dp = a.draws + p;
+            uint32_t        T  = 0;
+            for (uint32_t i0 = 0; i0 < a.spp; i0 += 8) {
+                uint32_t d[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d[j] = (px.inside && i0 + j < a.spp) ? (uint32_t)dp[(size_t)(i0 + j) * a.n_px] : 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t i = i0 + (uint32_t)j;
+                    if (i < a.spp && i % a.chunk_len == 0) {
+                        const uint32_t g = T ? (T - 1) / MT_N + 1 : 0u;
+                        const uint32_t w = T ? T - (g - 1) * MT_N : (uint32_t)MT_N;
+                        a.snap_ctl[(size_t)(i / a.chunk_len) * a.n_px + p] = w | (g << 16);
+                    }
+                    T += d[j];
+                }
+            }
+            if (px.inside) {
+                const uint32_t G = T ? (T - 1) / MT_N + 1 : 0u;
+#pragma unroll 1
+                for (uint32_t g = 0; g < G; ++g) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(rng, (int)g), mt_buf(rng, (int)g + 1));
+            }
+            continue;
+        }
         // hit records do not depend on the stream: load sample i + 1's while sample i is replayed
         float4 next = px.inside ? a.hits[p] : make_float4(0.0f, __uint_as_float(NO_HIT), 0.0f, 0.0f);
         for (uint32_t i = 0; i < a.spp; ++i) {
@@ -188,10 +219,6 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
             if (i % a.chunk_len == 0) // stream position at the start of chunk i / chunk_len
                 a.snap_ctl[(size_t)(i / a.chunk_len) * a.n_px + p] = (uint32_t)rng.idx | ((uint32_t)rng.cur << 16);
             if (!px.inside) continue;
-            if (a.draws) { // counts known from the camera pass: advance the stream only
-                rng_skip(rng, a.draws[(size_t)i * a.n_px + p]);
-                continue;
-            }
             rng_prepare(rng);
             const uint32_t code = __float_as_uint(rec.y);
             if (code == NO_HIT) continue;
