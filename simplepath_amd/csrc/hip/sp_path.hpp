@@ -116,8 +116,7 @@ struct Rng {
     // + 2 srv_dc + srv_coat (draw counts); glossy_weights takes them from srv_w when the stream is
     // exactly there.
     // srv_on: 0 off; 1 served weights available (srv_B: eval / pdf / sample of the light being
-    // estimated, srv_A: the bounce's own Material::sample at srv_posA); 2 defer the bounce's
-    // Material::sample estimate (glossy_weights records where it starts and skips its words).
+    // estimated, srv_A: the bounce's own deferred Material::sample, its estimate at srv_posA).
     int       srv_on  = 0;
     bool      srv_A = false, srv_B = false;
     uint32_t  srv_pos = 0, srv_dc = 0, srv_coat = 0, srv_posA = 0, srv_pwA = 0;
@@ -1645,20 +1644,6 @@ static __shared__ uint8_t srv_req[4][4 * 64]; // request r: owner lane | k << 6 
 __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
 {
 #if SP_SERVE_RHO
-    if (rng.srv_on == 2) {
-        // the bounce's Material::sample, deferred (integrate_rrnee): note where its estimate starts
-        // and skip the words; the weights {0, 1} pick the lambertian lobe, which draws the same
-        // three words after the estimate as either lobe can with the real weights (the glossy one
-        // draws none only when wo.y == 0, and then its weight is 0)
-        rng.srv_A    = true;
-        rng.srv_dc   = wo.y == 0.0f ? 0u : 32u;
-        rng.srv_posA = rng.draws;
-        rng.srv_pwA  = ((uint32_t)rng.cur << 16) | (uint32_t)rng.idx;
-        w[0]         = 0.0f;
-        w[1]         = 1.0f;
-        rng_skip_reserved(rng, (int)rng.srv_dc);
-        return;
-    }
     if (rng.srv_on == 1) {
         // the same estimate (same material, wo and stream words) was computed by the wave: take it
         // and advance the stream past its words
@@ -2358,25 +2343,36 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
                 n  = qr.is.n;
 #if SP_SERVE_SAMPLE
                 // The bounce's Material::sample estimate joins the first light's served estimates:
-                // its words are skipped now (placeholder weights, the same draw count) and the call
-                // is repeated from here with the served weights after the first light's shadow ray.
+                // the sample's words are skipped now and the call runs from here with the served
+                // weights after the first light's shadow ray.
                 // The whole bounce (at most 1 + 32 + 3 + 2 + 97 words up to that light's sample
                 // estimate) is reserved first, so none of these words is twisted over meanwhile.
-                const bool defer = c.sc.n_lights > 0;
+                const bool defer = c.sc.n_lights > 0 && material_has_rho(c.sc, qr.is.material);
                 if (defer) {
                     rng_reserve(c.rng, 140);
-                    snap         = c.rng;
-                    c.rng.srv_on = 2;
-                    c.rng.srv_A  = false;
+                    snap = c.rng;
+                    // material_sample_local's draws without its arithmetic: a clearcoat's Fresnel
+                    // pick first (a specular pick is drawn again below, from snap, and computed now)
+                    const Material& mm   = c.sc.materials[qr.is.material];
+                    const f3        wl   = to_onb(onb_from_v(n, c.q), wo);
+                    bool            spec = false;
+                    if (mm.kind == SP_MAT_CLEARCOAT) spec = next1D(c.rng) < fresnel_dielectric(wl.y, 1.0f, mm.coat_ior);
+                    if (spec) {
+                        c.rng = snap;
+                    } else {
+                        // the estimate starts here; after it the sample draws three words whichever
+                        // lobe it picks (the glossy lobe draws none only when wo.y == 0, and then its
+                        // weight is 0)
+                        pend           = true;
+                        c.rng.srv_dc   = (wl.y == 0.0f) ? 0u : 32u;
+                        c.rng.srv_posA = c.rng.draws;
+                        c.rng.srv_pwA  = ((uint32_t)c.rng.cur << 16) | (uint32_t)c.rng.idx;
+                        rng_skip_reserved(c.rng, (int)c.rng.srv_dc + 3);
+                    }
                 }
+                if (!pend)
 #endif
                 s = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
-#if SP_SERVE_SAMPLE
-                if (defer) {
-                    pend         = c.rng.srv_A; // the estimate was reached (a glossy base, no specular coat pick)
-                    c.rng.srv_on = 0;
-                }
-#endif
                 if (pend) hit = true; // whether the sample is usable is known once it is finished
                 else if (s.pdf == 0.0f || cblack(s.color)) alive = false;
                 else hit = true;
