@@ -7,6 +7,10 @@
 #endif
 #define SP_RNG_PF 0
 #define SP_RHO_TOUCH 1
+// Twist ahead at the bounce start once within 144 words of the end (the blocked twist, batched
+// over the wave), so the 140-word reservation of a served bounce (sp_path.hpp integrate_rrnee)
+// never falls back to the compact per-lane twist: 793-797 -> 810-822 Mrays/s on elf 1024^2 @ 16 spp.
+#define SP_RNG_MARGIN 144
 // The bounce's own Material::sample estimate joins the first light's served round (sp_path.hpp
 // integrate_rrnee): 768-775 -> 783-797 Mrays/s on elf 1024^2 @ 16 spp (profiles/r03/ab_rrnee_served.txt).
 #ifndef SP_SERVE_SAMPLE
