@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads for the CPU baseline (0 = this process's CPU share: OMP_NUM_THREADS when set, "
                          "else os.cpu_count())")
+    ap.add_argument("--cpu-scaling-seconds", type=float, default=3.0,
+                    help="N = 1: budget per leg of the reference's thread-scaling sample (1 thread and the CPU "
+                         "share); 0 = skip")
     ap.add_argument("--parity-seconds", type=float, default=6.0,
                     help="N > 1: CPU budget for the parity sample of the gathered frame")
     ap.add_argument("--pg-timeout", type=float, default=1800.0,
@@ -266,9 +269,11 @@ def main():
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    stats = []
+    stats, step_s = [], []
     for _ in range(args.steps):
-        stats.append(step())
+        ts = time.perf_counter()
+        stats.append(step())  # stage timing reads the render's events back: each step has finished here
+        step_s.append(time.perf_counter() - ts)
     sync()
     if dist is not None:
         dist.barrier()
@@ -320,6 +325,8 @@ def main():
         try:
             if world == 1:  # the CPU baseline is timed at N=1 only
                 cpu, parity = cpu_baseline(scene, path, integ, args, out, my_tiles, args.cpu_seconds)
+                if args.cpu_scaling_seconds > 0 and cpu is not None and cpu["kind"] == "reference":
+                    cpu["thread_scaling"] = cpu_thread_scaling(path, integ, args, my_tiles, cpu)
             else:  # parity of the GATHERED frame (all ranks' tiles, after the RCCL gather)
                 _, parity = cpu_baseline(scene, path, integ, args, frame, np.arange(n_tiles, dtype=np.int32),
                                          args.parity_seconds)
@@ -337,6 +344,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        # wall time of each timed step (rank 0; render + gather), to show run-to-run spread
+        "step_ms": {"min": round(min(step_s) * 1e3, 3), "max": round(max(step_s) * 1e3, 3)},
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -353,6 +362,8 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity,
+        # which library ran (SP_LIB_PATH can swap it): path, content hash of its sources, .so hash
+        "library": None if cpu_render else sp._abi.build_identity(),
     }
     if dist is not None:
         line["world_size"] = world
@@ -489,6 +500,62 @@ def _ref_lib():
     L.ref_render_tiles.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.POINTER(C.c_int32), C.c_int64, C.c_int,
                                    C.POINTER(C.c_float)]
     return L
+
+
+def cpu_thread_scaling(scene_path, integ, args, my_tiles, cpu):
+    """The reference's own thread scaling on this host: the same random tiles at 1 thread and at
+    the process's CPU share, a few seconds each.  The reference's default is hardware_concurrency()
+    threads (main.cpp:314); the GPU box's pool rules give one GPU's process a 16-CPU share although
+    the affinity mask shows the whole machine, so the whole-host rate is reported as a linear
+    extrapolation of the share's per-thread rate -- an upper bound, labelled as such, not a
+    measurement."""
+    import ctypes as C
+    ref = _ref_lib()
+    if ref is None:
+        return None
+    ref_scene = ref.ref_scene_create(scene_path.encode(), args.width, args.height)
+    if not ref_scene:
+        return None
+    order = np.random.default_rng(99).permutation(np.asarray(my_tiles)).astype(np.int32)
+    share = args.cpu_threads if args.cpu_threads > 0 else cpu_share()
+    from tests import _oracle
+    legs = {}
+    try:
+        for threads in sorted({1, share}):
+            done, t_used, chunk = 0, 0.0, threads
+            while t_used < args.cpu_scaling_seconds and done < order.size:
+                ids = np.ascontiguousarray(order[done:done + chunk])
+                out = np.zeros((ids.size, 64, 3), dtype=np.float32)
+                t0 = time.perf_counter()
+                rc = ref.ref_render_tiles(ref_scene, int(integ), args.spp, ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          ids.size, threads, out.ctypes.data_as(C.POINTER(C.c_float)))
+                t_used += time.perf_counter() - t0
+                assert rc == 0
+                done += ids.size
+                chunk *= 2
+            legs[threads] = (done, t_used)
+    finally:
+        ref.ref_scene_free(ref_scene)
+    # rays of each leg's tiles from the oracle (bit-exact twin of the reference)
+    res = {}
+    s = sp_scene_for(scene_path, args)
+    for threads, (done, t_used) in legs.items():
+        _, st = _oracle.render(s, integ, args.spp, np.ascontiguousarray(order[:done]), threads=share, variant="glibc")
+        res[threads] = {"tiles": done, "s": round(t_used, 2), "mrays_per_s": round(st["rays"] / t_used / 1e6, 4)}
+    one, sh = res[1]["mrays_per_s"], res[share]["mrays_per_s"]
+    host = affinity_cpus()
+    return {"legs": {str(k): v for k, v in res.items()},
+            "efficiency_at_share": round(sh / (one * share), 4) if one > 0 else None,
+            "full_host_threads": host,
+            "full_host_linear_estimate_mrays_per_s": round(sh / share * host, 3),
+            "note": "estimate, not a measurement: the box's CPU share is %d of %d CPUs" % (share, host)}
+
+
+def sp_scene_for(scene_path, args):
+    import simplepath_amd as sp
+    s = sp.Scene.from_file(scene_path)
+    s.set_resolution(args.width, args.height)
+    return s
 
 
 def cpu_baseline(scene, scene_path, integ, args, gpu_out, my_tiles, budget_s):

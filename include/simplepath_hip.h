@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 4
+#define SP_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------------- */
 enum {
@@ -183,7 +183,10 @@ typedef struct sp_scene_desc {
  * tile list on the device (d_tile_ids) or absent, sp_render_tiles only enqueues work on `stream`
  * and returns -- two calls and a dependent kernel can be queued back to back with no host wait.
  * Requesting stats waits for the render (the counters are read back).  Calls on one scene share
- * its device scratch, so they must be ordered on one stream (or the host must wait in between). */
+ * its device scratch; they may come from several host threads and streams (the reference's
+ * render() shares one Scene across threads, main.cpp:122-130): the scene serialises them, on the
+ * host with a per-scene lock and on the device by making each call's stream wait for the previous
+ * call's work (ABI 5).  A host tile list is copied before the call returns. */
 typedef struct sp_render_params {
     int32_t        integrator;        /* SP_INTEGRATOR_*; 0 => scene's (DirectLighting if unset: main.cpp:387-392) */
     uint32_t       samples_per_pixel; /* main.cpp `--samples`                                    */
@@ -194,8 +197,8 @@ typedef struct sp_render_params {
     int32_t        flags;             /* SP_PIPELINE_* (0 = automatic) | SP_RENDER_STAGE_TIMING   */
     /* ---- ABI 4 ---- */
     const int32_t* d_tile_ids;        /* DEVICE array of num_tiles tile indices, used when tile_ids is
-                                         NULL: not copied or checked on the host (an id outside the
-                                         image renders as zeros)                                  */
+                                         NULL: not copied or checked on the host (an id outside
+                                         [0, tiles) -- negative ones included -- renders as zeros) */
     int32_t        waves_per_simd;    /* megakernel occupancy (__launch_bounds__ variant): 0 = automatic
                                          (DirectLighting 4, IterativeRRNEE 3, fewer if the LDS caps it);
                                          else DirectLighting 1-4, IterativeRRNEE 2-4               */
@@ -204,7 +207,12 @@ typedef struct sp_render_params {
     float          chunk_max_gb;      /* sample-chunk buffer budget in GB: 0 = 96, never more than the
                                          device's free memory; AUTO falls back to the megakernel when
                                          the buffers do not fit                                    */
-    int32_t        reserved[3];       /* must be 0                                                  */
+    /* ---- ABI 5 ---- */
+    float          tile_order_factor; /* megakernel tile order (DirectLighting, IterativeRRNEE): 0 =
+                                         automatic (a one-sample probe times every tile and tiles
+                                         slower than 2x the mean go first, from 6 tiles per wave and
+                                         128 spp); > 0: always, with this factor; < 0: queue order  */
+    int32_t        reserved[2];       /* must be 0                                                  */
 } sp_render_params;
 
 /* Device pipeline selection (sp_render_params.flags).  All produce identical images. */
@@ -265,6 +273,8 @@ typedef struct sp_bvh_info {
 typedef struct sp_scene sp_scene;
 
 const char* sp_version(void);
+/* ABI 5: content hash (16 hex digits) of the sources, headers and flags the library was built from. */
+const char* sp_build_id(void);
 const char* sp_last_error(void);
 
 int  sp_string_to_integrator(const char* name, int32_t* out);

@@ -188,7 +188,8 @@ STAGE_TIMING = 4  # SP_RENDER_STAGE_TIMING
 
 
 def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeline="auto",
-            stage_timing=False, waves_per_simd=0, chunks_per_pixel=0, chunk_max_gb=0.0) -> tuple:
+            stage_timing=False, waves_per_simd=0, chunks_per_pixel=0, chunk_max_gb=0.0,
+            tile_order_factor=0.0) -> tuple:
     if isinstance(integrator, str):
         integrator = string_to_integrator_type(integrator)
     p = _abi.sp_render_params()
@@ -204,6 +205,7 @@ def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeli
     p.waves_per_simd = int(waves_per_simd)
     p.chunks_per_pixel = int(chunks_per_pixel)
     p.chunk_max_gb = float(chunk_max_gb)
+    p.tile_order_factor = float(tile_order_factor)
     return p, keep
 
 
@@ -215,7 +217,8 @@ def _stats(s: _abi.sp_render_stats) -> RenderStats:
 def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Optional[Sequence[int]] = None,
                  pipeline="auto", **options):
     """Render tiles on the GPU; returns (tile-packed radiance [n,64,3] float32, RenderStats).
-    options: waves_per_simd, chunks_per_pixel, chunk_max_gb (sp_render_params, ABI 4)."""
+    options: waves_per_simd, chunks_per_pixel, chunk_max_gb (sp_render_params, ABI 4),
+    tile_order_factor (ABI 5: 0 automatic, > 0 forced with that factor, < 0 queue order)."""
     p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids),
                       pipeline=pipeline, **options)
     n = keep.size if keep is not None else TileScheduler(scene.width, scene.height).get_num_tiles()
@@ -230,8 +233,8 @@ def render_tiles_device(scene: Scene, integrator, num_pixel_samples: int, tile_i
                         num_tiles: int = 0, **options):
     """Render into a caller-owned device buffer (e.g. a torch.cuda tensor's data_ptr()).
     tile_ids: host tile list (None: d_tile_ids, a device pointer to num_tiles int32 ids, or every
-    tile).  With stats=False (and no stage timing, no host tile list) the render is only enqueued
-    on `stream`: the call returns without waiting (returns None)."""
+    tile).  With stats=False (and no stage timing) the render is only enqueued on `stream`: the
+    call returns without waiting (returns None); a host tile list is copied before it returns."""
     p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids), stream,
                       pipeline, stage_timing, **options)
     if d_tile_ids:

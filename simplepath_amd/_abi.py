@@ -94,7 +94,9 @@ class sp_render_params(C.Structure):
         ("stream", C.c_void_p), ("bvh_mode", C.c_int32), ("flags", C.c_int32),
         # ABI 4
         ("d_tile_ids", C.c_void_p), ("waves_per_simd", C.c_int32), ("chunks_per_pixel", C.c_int32),
-        ("chunk_max_gb", C.c_float), ("reserved", C.c_int32 * 3),
+        ("chunk_max_gb", C.c_float),
+        # ABI 5
+        ("tile_order_factor", C.c_float), ("reserved", C.c_int32 * 2),
     ]
 
 
@@ -122,6 +124,7 @@ class sp_bvh_info(C.Structure):
 # Every symbol declared in include/simplepath_hip.h, with its ctypes signature.
 SIGNATURES = {
     "sp_version": (C.c_char_p, []),
+    "sp_build_id": (C.c_char_p, []),
     "sp_last_error": (C.c_char_p, []),
     "sp_string_to_integrator": (C.c_int, [C.c_char_p, C.POINTER(C.c_int32)]),
     "sp_scene_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
@@ -169,6 +172,19 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def build_identity() -> dict:
+    """Which library this process runs: its path, the build's content hash (sp_build_id, ABI 5)
+    and the SHA-256 prefix of the .so file itself -- recorded in every bench line, so a swapped
+    library (SP_LIB_PATH) is visible."""
+    import hashlib
+    L = lib()
+    with open(LIB_PATH, "rb") as f:
+        so_sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    return {"path": os.path.relpath(os.path.realpath(LIB_PATH), os.path.dirname(_HERE)),
+            "build_id": L.sp_build_id().decode(), "so_sha256_16": so_sha,
+            "default": os.path.realpath(LIB_PATH) == os.path.realpath(os.path.join(_HERE, "_build", "libsimplepath_hip.so"))}
 
 
 class SimplePathError(RuntimeError):

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -19,6 +20,7 @@ namespace spd {
 hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
+size_t     render_static_lds(int integ, int variant);
 hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream);
 bool       has_probe(int integ);
 hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
@@ -236,6 +238,19 @@ struct sp_scene {
     int32_t*             d_order     = nullptr;
     size_t               order_cap   = 0;
     unsigned long long*  probe_counters = nullptr;
+    // One scene, many host threads (the reference's render() shares one Scene across N threads,
+    // main.cpp:122-130): the render scratch above is per scene, so calls are serialised -- on the
+    // host by `mu`, and on the device by making each call's stream wait for the previous call's
+    // last operation (ev_done), whichever stream that call used.  A host tile list is staged
+    // through pinned memory (h_tiles) whose previous copy is waited for before it is rewritten, so
+    // the caller's array may be reused as soon as sp_render_tiles returns.
+    std::mutex           mu;
+    hipEvent_t           ev_done  = nullptr; // recorded at the end of every render call
+    bool                 done_rec = false;
+    int32_t*             h_tiles  = nullptr; // pinned staging of host tile lists
+    size_t               h_tiles_cap = 0;
+    hipEvent_t           ev_tiles = nullptr; // after the staged copy
+    bool                 tiles_rec = false;
 
     void release()
     {
@@ -277,6 +292,10 @@ struct sp_scene {
         if (d_order) (void)hipFree(d_order);
         if (probe_counters) (void)hipFree(probe_counters);
         d_tile_time = nullptr; d_order = nullptr; order_cap = 0; probe_counters = nullptr;
+        if (ev_done) (void)hipEventDestroy(ev_done);
+        if (ev_tiles) (void)hipEventDestroy(ev_tiles);
+        if (h_tiles) (void)hipHostFree(h_tiles);
+        ev_done = ev_tiles = nullptr; done_rec = tiles_rec = false; h_tiles = nullptr; h_tiles_cap = 0;
         mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
         ev0 = ev1 = ev_render = nullptr;
         mt_waves = 0; d_tiles_cap = 0;
@@ -375,6 +394,9 @@ int wrap_load(std::unique_ptr<sph::Scene> (*fn)(const std::string&, const std::s
 extern "C" {
 
 const char* sp_version(void) { return "simplepath-amd 0.1 (gfx950)"; }
+// content hash of the sources and flags of this build (simplepath_amd/Makefile, ABI 5)
+extern const char* const sp_build_id_str;
+const char* sp_build_id(void) { return sp_build_id_str; }
 const char* sp_last_error(void) { return g_last_error.c_str(); }
 
 int sp_string_to_integrator(const char* name, int32_t* out)
@@ -860,6 +882,8 @@ static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params
     SP_HIP(hipMalloc(&s->counters, 8 * sizeof(unsigned long long)));
     SP_HIP(hipEventCreate(&s->ev0));
     SP_HIP(hipEventCreate(&s->ev1));
+    SP_HIP(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
+    SP_HIP(hipEventCreateWithFlags(&s->ev_tiles, hipEventDisableTiming));
     return SP_OK;
 }
 
@@ -867,6 +891,8 @@ static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params
 // come back as error codes with sp_last_error() set.
 int sp_scene_upload_ex(sp_scene* s, int32_t device, const sp_upload_params* params)
 {
+    if (!s) return fail(SP_ERR_ARG, "null scene");
+    std::lock_guard<std::mutex> lock(s->mu);
     try {
         return scene_upload_impl(s, device, params);
     } catch (const sph::SpError& e) {
@@ -886,6 +912,8 @@ int sp_scene_upload(sp_scene* s, int32_t device, int32_t bvh_mode)
 static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats);
 int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats)
 {
+    if (!s) return fail(SP_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lock(s->mu); // calls on one scene run one at a time (sp_scene::mu)
     try {
         return render_tiles_impl(s, p, d_out, stats);
     } catch (const sph::SpError& e) {
@@ -944,6 +972,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     if (p->tile_ids && p->d_tile_ids) return fail(SP_ERR_ARG, "give tile_ids (host) or d_tile_ids (device), not both");
     if (p->chunks_per_pixel < 0) return fail(SP_ERR_ARG, "chunks_per_pixel < 0");
     if (!(p->chunk_max_gb >= 0.0f)) return fail(SP_ERR_ARG, "chunk_max_gb < 0");
+    if (p->tile_order_factor != p->tile_order_factor) return fail(SP_ERR_ARG, "tile_order_factor is NaN");
     if ((p->flags & ~(3 | SP_RENDER_STAGE_TIMING)) != 0) return fail(SP_ERR_ARG, "unknown flags");
     SP_HIP(hipSetDevice(s->device));
     int32_t integ = p->integrator;
@@ -970,6 +999,9 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     hipStream_t stream = static_cast<hipStream_t>(p->stream);
     if (stats) *stats = sp_render_stats{};
     if (n_tiles == 0) return SP_OK;
+    // the previous call on this scene may have used another stream: its work on the shared
+    // scratch comes first (sp_scene::mu)
+    if (s->done_rec) SP_HIP(hipStreamWaitEvent(stream, s->ev_done, 0));
     const int32_t* d_ids = p->d_tile_ids; // device tile list (nullptr: slot = tile)
     if (p->tile_ids) {
         if ((size_t)n_tiles > s->d_tiles_cap) {
@@ -978,7 +1010,19 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             SP_HIP(hipMalloc(&s->d_tiles, (size_t)n_tiles * sizeof(int32_t)));
             s->d_tiles_cap = (size_t)n_tiles;
         }
-        SP_HIP(hipMemcpyAsync(s->d_tiles, p->tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+        // staged through pinned memory, so the caller's array is free once this returns
+        if (s->tiles_rec) SP_HIP(hipEventSynchronize(s->ev_tiles)); // the previous staged copy is done
+        if ((size_t)n_tiles > s->h_tiles_cap) {
+            if (s->h_tiles) (void)hipHostFree(s->h_tiles);
+            s->h_tiles     = nullptr;
+            s->h_tiles_cap = 0;
+            SP_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_tiles), (size_t)n_tiles * sizeof(int32_t), hipHostMallocDefault));
+            s->h_tiles_cap = (size_t)n_tiles;
+        }
+        std::memcpy(s->h_tiles, p->tile_ids, (size_t)n_tiles * sizeof(int32_t));
+        SP_HIP(hipMemcpyAsync(s->d_tiles, s->h_tiles, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+        SP_HIP(hipEventRecord(s->ev_tiles, stream));
+        s->tiles_rec = true;
         d_ids = s->d_tiles;
     }
     if (s->n_cu == 0) {
@@ -1204,13 +1248,17 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     } else {
         const int    rs_words  = spd::rsqrt_words(s->dev);
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;
-        if (lds_bytes > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+        // the kernel's static LDS counts too (the largest over the variants this call may pick)
+        size_t lds_static = 0;
+        for (int v = 2; v <= 4; ++v) lds_static = std::max(lds_static, spd::render_static_lds(integ, v));
+        const size_t lds_all = lds_bytes + lds_static;
+        if (lds_all > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
         // waves per SIMD the kernel is compiled for (SP_KERNEL_VARIANT): DirectLighting 4,
         // IterativeRRNEE 3 -- but never more than the LDS lets run (one 4-wave block per wave per
         // SIMD): a deep BVH's stacks (lucy: 3 blocks per CU) would leave the extra occupancy's
         // register budget paid for in spills and unused (lucy 1080p @ 256 spp: 2007 Mrays/s at 3
         // waves, 1879 at 4; profiles/r02/s5)
-        const int lds_waves = (int)std::min<size_t>(8, (160 * 1024) / lds_bytes);
+        const int lds_waves = (int)std::min<size_t>(8, (160 * 1024) / lds_all);
         int       variant   = integ == SP_INTEGRATOR_ITERATIVE_RRNEE ? 3 : 4;
         variant             = std::max(2, std::min(variant, lds_waves));
         if (waves_req) variant = waves_req;
@@ -1272,10 +1320,10 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // frame -- bunny 1080p @ 256 spp (7.9 tiles per wave) +3-4 %, lucy +2 %, elf's 8-way
         // shard +3 %; spheres 1024^2 (4 tiles per wave) lost 1 % at 256 spp and 5 % at 64 spp.
         // DirectLighting and IterativeRRNEE have probe kernels (sp_probe_*.hip); the other
-        // integrators render in queue order.  SP_TILE_HOIST=<factor> forces it (test hook; 0 =
-        // queue order).
+        // integrators render in queue order.  sp_render_params.tile_order_factor > 0 forces it with
+        // that factor, < 0 turns it off.
         float hoist = (n_tiles >= 6 * (int64_t)waves && p->samples_per_pixel >= 128) ? 2.0f : 0.0f;
-        if (const char* v = std::getenv("SP_TILE_HOIST")) hoist = (float)std::atof(v);
+        if (p->tile_order_factor != 0.0f) hoist = std::max(0.0f, p->tile_order_factor);
         if (hoist > 0.0f && n_tiles > (int64_t)waves && spd::has_probe(integ)) {
             if ((size_t)n_tiles > s->order_cap) {
                 if (s->d_tile_time) (void)hipFree(s->d_tile_time);
@@ -1317,6 +1365,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         launches += 1;
     }
     SP_HIP(hipEventRecord(s->ev1, stream));
+    SP_HIP(hipEventRecord(s->ev_done, stream));
+    s->done_rec = true;
     // stream order: without stats nothing waits -- the render is only enqueued
     if (stats) {
         SP_HIP(hipEventSynchronize(s->ev1));

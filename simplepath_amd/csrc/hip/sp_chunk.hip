@@ -72,7 +72,7 @@ __device__ __forceinline__ Px pixel(const Scene& sc, const ChunkArgs& a, int64_t
     Px            p;
     p.x      = (uint32_t)((tile % a.tiles_x) * 8) + morton_decode_1(lane);
     p.y      = (uint32_t)((tile / a.tiles_x) * 8) + morton_decode_1(lane >> 1);
-    p.inside = (int)p.x < sc.width && (int)p.y < sc.height;
+    p.inside = p.x < (uint32_t)sc.width && p.y < (uint32_t)sc.height; // unsigned: a negative id is outside
     return p;
 }
 

@@ -114,6 +114,15 @@ hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float fact
     return hipGetLastError();
 }
 
+// Static LDS of a render kernel (libm tables, the rho sink, IterativeRRNEE's served-estimate
+// rows): the 160 KB guard and the LDS occupancy cap count it beside the dynamic part.
+size_t render_static_lds(int integ, int variant)
+{
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(select_kernel(integ, variant))) != hipSuccess) return 0;
+    return fa.sharedSizeBytes;
+}
+
 int render_blocks_per_cu(int integ, int variant, size_t lds_bytes)
 {
     int n = 0;

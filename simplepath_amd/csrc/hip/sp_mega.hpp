@@ -61,7 +61,8 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
         const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
         const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
-        const bool     inside = (int)px < sc.width && (int)py < sc.height;
+        // unsigned compares: a negative tile id (device lists are not checked) lands outside
+        const bool     inside = px < (uint32_t)sc.width && py < (uint32_t)sc.height;
         rgb            acc    = mkc(0, 0, 0);
         uint64_t       prof[4] = { 0, 0, 0, 0 };
         if (inside) {

@@ -2288,8 +2288,13 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int total = 3 * __popcll(mb) + __popcll(ma);
-    for (int r0 = 0; r0 < total; r0 += 64) {
-        const int      r = r0 + lane;
+    // requests are dealt to the lanes that are here: on a clipped border tile the pixels outside
+    // the image never enter integrate(), so lane ids are not request slots -- rank the active lanes
+    const uint64_t act  = __ballot(1);
+    const int      rank = __popcll(act & ((1ull << lane) - 1ull));
+    const int      nact = __popcll(act);
+    for (int r0 = 0; r0 < total; r0 += nact) {
+        const int      r = r0 + rank;
         const uint32_t e = (r < total) ? (uint32_t)srv_req[wave][r] : 0u;
         const int      o = (int)(e & 63u), k = (int)(e >> 6);
         // the owner's inputs (all lanes take part in the exchange)

@@ -94,7 +94,7 @@ __device__ __forceinline__ PixelRef pixel_of(const Scene& sc, const WaveArgs& w,
     PixelRef       r;
     r.px     = (uint32_t)((tile % w.tiles_x) * 8) + morton_decode_1(lane);
     r.py     = (uint32_t)((tile / w.tiles_x) * 8) + morton_decode_1(lane >> 1);
-    r.inside = (int)r.px < sc.width && (int)r.py < sc.height;
+    r.inside = r.px < (uint32_t)sc.width && r.py < (uint32_t)sc.height; // unsigned: a negative id is outside
     return r;
 }
 
@@ -428,17 +428,10 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_stats(WaveArgs w, int64_t n_slots
 // ---------------------------------------------------------------------------- host side
 // wf_shadow's LDS: per-wave any-hit stacks (wide-BVH depth, not the binary closest-hit depth)
 static size_t wave_shadow_lds(const Scene& sc) { return (size_t)(WF_BLOCK / 64) * sc.any_stack_words * 64 * 4; }
-static int shade_waves_env()
-{
-    const char* v = std::getenv("SP_SHADE_WAVES");
-    return v ? std::atoi(v) : 5; // 4 / 5 / 6 waves: 2280 / 2306 / 2236 Mrays/s (profiles/r02/s5)
-}
-static int32_t interleave_block_env()
-{
-    const char* v = std::getenv("SP_WAVE_ILV");
-    const int   b = v ? std::atoi(v) : 240; // one 1080p tile row (profiles/r01 sweep: 1..16200 within 3%)
-    return b > 0 ? b : 240;
-}
+// shading kernel occupancy: 4 / 5 / 6 waves per SIMD measured 2280 / 2306 / 2236 Mrays/s (profiles/r02/s5)
+static int shade_waves_env() { return 5; }
+// tiles per interleave block of the two parts: one 1080p tile row (profiles/r01 sweep: 1..16200 within 3 %)
+static int32_t interleave_block_env() { return 240; }
 static uint32_t diag_sample_env()
 {
     const char* v = std::getenv("SP_WAVE_DIAG_SAMPLE");

@@ -224,7 +224,6 @@ Bvh build_bvh_sah(const std::vector<PrimBounds>& bounds, int max_leaf)
 {
     Bvh        out;
     SahBuilder b{ bounds, {}, {}, {}, {}, {}, max_leaf };
-    if (const char* v = std::getenv("SP_SAH_CT")) b.trav_cost = (float)std::atof(v); // tuning knob
     const size_t n = bounds.size();
     b.ids.resize(n);
     b.cx.resize(n); b.cy.resize(n); b.cz.resize(n);

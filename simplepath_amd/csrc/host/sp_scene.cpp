@@ -672,9 +672,10 @@ private:
         }
     }
 
-    // m_materials.find + LOG_ERROR (base/FileParser.cpp:494-498, 555-559): an unknown name is
-    // reported and parsing goes on; the block's own check ("needs a base material" / "needs a
-    // material") then fails
+    // m_materials.find + LOG_ERROR (base/FileParser.cpp:494-498, 555-559, 660-665): an unknown name
+    // is reported and parsing goes on with the block's material left as it was (-1 on a miss), so an
+    // earlier valid name stays; the block's own check ("needs a base material" / "needs a
+    // material") fails only when none was found
     int find_material(const std::string& name)
     {
         for (size_t i = 0; i < m_scene->material_names.size(); ++i)
@@ -810,7 +811,7 @@ private:
         rgb         color = mkc(1, 1, 1);
         attributes(body, "material_clearcoat", [&](const std::string& w, Cursor& c) {
             if (w == "name") name = trim_char(c.get_word(), '"');
-            else if (w == "base") base = find_material(trim_char(c.get_word(), '"'));
+            else if (w == "base") { if (const int m = find_material(trim_char(c.get_word(), '"')); m >= 0) base = m; }
             else if (w == "color") { f3 v = c.get_vec3(); color = mkc(v.x, v.y, v.z); }
             else if (w == "ior") ior = c.get_float();
             else return false;
@@ -872,7 +873,7 @@ private:
         int         material = -1;
         std::string path;
         attributes(body, "mesh", [&](const std::string& w, Cursor& c) {
-            if (w == "material") material = find_material(trim_char(c.get_word(), '"'));
+            if (w == "material") { if (const int m = find_material(trim_char(c.get_word(), '"')); m >= 0) material = m; }
             else if (w == "file") path = c.get_path();
             else if (w == "translate") append_translate(xf, c.get_vec3());
             else if (w == "rotate") { f3 a = c.get_vec3(); float d = c.get_float(); append_rotate(xf, a, d); }
@@ -905,7 +906,7 @@ private:
         AffXf xf{ aff_identity(), aff_identity() };
         int   material = -1;
         attributes(body, kind == SP_PRIM_PLANE ? "plane" : "sphere", [&](const std::string& w, Cursor& c) {
-            if (w == "material") material = find_material(trim_char(c.get_word(), '"'));
+            if (w == "material") { if (const int m = find_material(trim_char(c.get_word(), '"')); m >= 0) material = m; }
             else if (w == "translate") append_translate(xf, c.get_vec3());
             else if (w == "rotate") { f3 a = c.get_vec3(); float d = c.get_float(); append_rotate(xf, a, d); }
             else if (w == "scale") append_scale(xf, c.get_vec3());

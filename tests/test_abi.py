@@ -54,12 +54,14 @@ def test_render_requires_upload(scene_dir):
 
 def test_abi_version_and_struct_layout():
     # ABI 4: sp_render_params grew the device tile list, occupancy and chunk fields; the ctypes
-    # mirror must match the header's layout
+    # mirror must match the header's layout.  ABI 5 (same layout): sp_build_id, per-scene
+    # serialisation of renders.
     import ctypes as C
     text = open(HEADER).read()
-    assert re.search(r"#define SP_ABI_VERSION 4\b", text)
+    assert re.search(r"#define SP_ABI_VERSION 5\b", text)
     assert C.sizeof(_abi.sp_render_params) == 72  # gcc on include/simplepath_hip.h: 72, 40, 60, 32
-    assert _abi.sp_render_params.d_tile_ids.offset == 40 and _abi.sp_render_params.reserved.offset == 60
+    assert _abi.sp_render_params.d_tile_ids.offset == 40 and _abi.sp_render_params.tile_order_factor.offset == 60
+    assert _abi.sp_render_params.reserved.offset == 64
     assert C.sizeof(_abi.sp_upload_params) == 32
 
 
@@ -74,3 +76,11 @@ def test_upload_params_validated_before_the_device(scene_dir):
     p = _abi.sp_upload_params()
     p.reserved = 3
     assert _abi.lib().sp_scene_upload_ex(scene.handle, 0, C.byref(p)) == _abi.SP_ERR_ARG
+
+
+def test_build_identity():
+    # the bench records which library ran: path, content hash of its sources, hash of the .so
+    ident = _abi.build_identity()
+    assert re.fullmatch(r"[0-9a-f]{16}", ident["build_id"]), ident
+    assert re.fullmatch(r"[0-9a-f]{16}", ident["so_sha256_16"]), ident
+    assert ident["path"].endswith("libsimplepath_hip.so")

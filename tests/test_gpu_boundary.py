@@ -145,22 +145,77 @@ def test_upload_options_are_part_of_the_residency(scene_dir):
 
 
 @pytest.mark.parametrize("integrator", ["direct_lighting", "iterative_rrnee", "whitted"])
-def test_tile_order_probe_is_invisible(scene_dir, monkeypatch, integrator):
+def test_tile_order_probe_is_invisible(scene_dir, integrator):
     # the megakernel's tile order (a one-sample probe pass, then the slow tiles first) changes only
     # which wave renders which tile and when: images and ray / draw counts equal queue order's,
     # also for a tile subset in a shuffled order
     s = load(scene_dir, "bunny.sp", 640, 512)  # 5120 tiles: more than the persistent waves (4096)
-    monkeypatch.setenv("SP_TILE_HOIST", "2")    # forced: AUTO uses it from 6 tiles per wave and 128 spp
-    ref, rst = sp.render_tiles(s, integrator, 2, pipeline="megakernel")
+    # forced (tile_order_factor): AUTO uses it from 6 tiles per wave and 128 spp
+    ref, rst = sp.render_tiles(s, integrator, 2, pipeline="megakernel", tile_order_factor=2.0)
     # probe, partition, render; integrators without a probe kernel (sp_probe_*.hip) keep queue order
     assert rst.launches == (1 if integrator == "whitted" else 3)
-    monkeypatch.setenv("SP_TILE_HOIST", "0")
-    off, ost = sp.render_tiles(s, integrator, 2, pipeline="megakernel")
+    off, ost = sp.render_tiles(s, integrator, 2, pipeline="megakernel", tile_order_factor=-1.0)
     assert ost.launches == 1
     assert np.array_equal(ref.view(np.uint32), off.view(np.uint32))
     assert (rst.rays, rst.shadow_rays, rst.samples, rst.rng_draws) == (ost.rays, ost.shadow_rays, ost.samples, ost.rng_draws)
-    for factor in ("0.5", "1.0", "4.0"):
-        monkeypatch.setenv("SP_TILE_HOIST", factor)
-        ids = np.random.default_rng(int(float(factor) * 10)).permutation(ref.shape[0]).astype(np.int32)
-        sub, _ = sp.render_tiles(s, integrator, 2, ids, pipeline="megakernel")
+    for factor in (0.5, 1.0, 4.0):
+        ids = np.random.default_rng(int(factor * 10)).permutation(ref.shape[0]).astype(np.int32)
+        sub, _ = sp.render_tiles(s, integrator, 2, ids, pipeline="megakernel", tile_order_factor=factor)
         assert np.array_equal(sub.view(np.uint32), ref[ids].view(np.uint32)), factor
+
+
+@pytest.mark.parametrize("pipeline", ["megakernel", "chunks", "wavefront"])
+def test_device_ids_outside_the_image_render_zeros(scene_dir, pipeline):
+    # a device tile list is not checked on the host: ids outside [0, tiles) -- negative ones too --
+    # render as zeros and add nothing to the ray counts
+    s = load(scene_dir, "bunny.sp", 72, 40, bvh=1)
+    n = sp.TileScheduler(72, 40).get_num_tiles()
+    good = np.array([3, 0, n - 1], dtype=np.int32)
+    ref, rst = sp.render_tiles(s, "direct_lighting", 3, good, pipeline=pipeline)
+    ids = np.array([3, -1, 0, n, -n, n - 1, -9], dtype=np.int32)
+    d = torch.from_numpy(ids).cuda()
+    out = torch.full((ids.size, 64, 3), 7.0, dtype=torch.float32, device="cuda:0")
+    st = sp.render_tiles_device(s, "direct_lighting", 3, None, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                pipeline=pipeline, d_tile_ids=d.data_ptr(), num_tiles=ids.size)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    valid = [0, 2, 5]
+    assert np.array_equal(o[valid].view(np.uint32), ref.view(np.uint32))
+    assert not o[[1, 3, 4, 6]].any()
+    assert (st.rays, st.shadow_rays, st.samples) == (rst.rays, rst.shadow_rays, rst.samples)
+
+
+@pytest.mark.parametrize("integrator", ["direct_lighting", "iterative_rrnee"])
+def test_one_scene_two_threads_two_streams(scene_dir, integrator):
+    # the reference's render() shares one Scene across host threads (main.cpp:122-130); two threads
+    # render disjoint tile sets of one scene on two streams without waiting (stats off) -- the
+    # scene serialises them, and each result equals a single-threaded call bit for bit
+    import threading
+    s = load(scene_dir, "bunny.sp", 160, 96)
+    n = sp.TileScheduler(160, 96).get_num_tiles()
+    sets = [np.arange(0, n, 2, dtype=np.int32), np.arange(1, n, 2, dtype=np.int32)]
+    refs = [sp.render_tiles(s, integrator, 4, ids, pipeline="megakernel")[0] for ids in sets]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.zeros((ids.size, 64, 3), dtype=torch.float32, device="cuda:0") for ids in sets]
+    errors = []
+    torch.cuda.synchronize()
+
+    def work(k):
+        try:
+            for _ in range(3):
+                ids = sets[k].copy()
+                sp.render_tiles_device(s, integrator, 4, ids, outs[k].data_ptr(), streams[k].cuda_stream,
+                                       pipeline="megakernel", stats=False)
+                ids[:] = -5  # the host list may be reused as soon as the call returns
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(2):
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), refs[k].view(np.uint32)), k

@@ -287,3 +287,17 @@ def test_forced_stackless_walk(scene_dir, monkeypatch, scene, w, h, integrator):
     assert ast.stack_depth == 0 and bst.stack_depth > 0
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
     assert (ast.rays, ast.shadow_rays, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.rng_draws)
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [("elf_small.sp", 70, 35, 3), ("material_spheres.sp", 70, 35, 3),
+                                           ("bunny.sp", 37, 21, 2)])
+def test_rrnee_clipped_border_tiles_bitexact(scene_dir, scene, w, h, spp):
+    # IterativeRRNEE with estimates served across the wave on image sizes that are not multiples
+    # of 8: the lanes of a border tile that fall outside the image never enter integrate(), so the
+    # served requests must be dealt to the lanes that are there (sp_path.hpp serve_rho)
+    s = load(scene_dir, scene, w, h, bvh=1)
+    g, gst = sp.render_tiles(s, "iterative_rrnee", spp)
+    c, cst = _oracle.render(s, sp.string_to_integrator_type("iterative_rrnee"), spp, variant="spm")
+    assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
+    assert np.isfinite(g).all()
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)

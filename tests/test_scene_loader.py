@@ -254,3 +254,45 @@ def test_scene_from_desc_validates(scene_dir):
     with pytest.raises(sp.SimplePathError) as e:
         sp.Scene.from_desc(d)
     assert e.value.code == -3 and "vertex index" in str(e.value)
+
+
+def test_unknown_material_name_keeps_the_earlier_one(capfd):
+    # m_materials.find misses leave the block's pointer as it was (base/FileParser.cpp:494-498,
+    # 555-559, 660-665): a later unknown name is logged and does not undo an earlier valid one
+    text = ("version: 1\n" + CAM + 'material_lambertian {\n name: "red"\n diffuse: 0.8 0.1 0.1\n}\n'
+            'material_lambertian {\n name: "blue"\n diffuse: 0.1 0.1 0.8\n}\n'
+            'material_clearcoat {\n name: "coat"\n base: "blue"\n base: "nope"\n}\n'
+            'sphere {\n material: "red"\n material: "missing"\n}\n'
+            'sphere {\n material: "coat"\n translate: 3 0 0\n}\n')
+    s = sp.Scene.from_string(text)
+    err = capfd.readouterr().err
+    assert "Material 'nope' not found" in err and "Material 'missing' not found" in err
+    d = s.desc()
+    mats = [d.shapes[k].material for k in range(2)]
+    assert mats == [0, 2]                   # red; the clearcoat
+    assert d.materials[2].base == 1         # blue survives the unknown "nope"
+
+
+def test_render_calls_from_many_threads_fail_cleanly(scene_dir):
+    # sp_render_tiles serialises calls on one scene (a per-scene lock): hammered from 8 threads
+    # before any upload, every call reports SP_ERR_STATE with its own thread-local message
+    import threading
+    from simplepath_amd import _abi
+    s = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp"))
+    codes, msgs = [], []
+
+    def work():
+        for _ in range(200):
+            try:
+                sp.render_tiles(s, "direct_lighting", 1, [0, 1])
+            except sp.SimplePathError as e:
+                codes.append(e.code)
+                msgs.append(str(e))
+
+    th = [threading.Thread(target=work) for _ in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert len(codes) == 1600 and set(codes) == {_abi.SP_ERR_STATE}
+    assert all("sp_scene_upload must be called" in m or "before rendering" in m for m in msgs)
