@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""TEST INFRASTRUCTURE: golden tiles of the full-size lucy.sp and elf.sp configs, rendered by the
+"""TEST INFRASTRUCTURE: golden tiles of the full-size bunny.sp, lucy.sp, elf.sp and material_spheres.sp configs, rendered by the
 reference itself (oracle/_ref/libsp_ref.so = the reference's Scene / BVHAccelerator / integrators
 compiled from /root/reference, driven by main.cpp:86-103's per-pixel loop).
 
@@ -12,6 +12,11 @@ tiles is rendered at the config's spp:
   2. tiles are picked from the probe: silhouettes (a mix of environment-only pixels and geometry),
      the highest-contrast all-geometry tiles (drapery folds, floor contact and shadows), and
      random tiles (seeded);
+     For bunny.sp (configs[2], the headline frame) the slowest tiles are added: every tile of the
+     frame is timed on the reference at 16 spp (the smaller of two runs), one thread per tile (8 worker
+     processes), and
+     the slowest whole tiles are taken -- the bunnies' undersides against the glossy floor, where
+     the deepest traversals and most of the glossy estimates sit;
   3. those tiles are rendered at the config's spp and stored with the mesh generator's
      parameters and the SHA-256 of the generated mesh file, so a test can prove it rebuilt the
      same scene before comparing, and with this CPU's RSQRTSS table: the reference normalises
@@ -21,8 +26,8 @@ tiles is rendered at the config's spp:
 Run in the build container (the reference sources are needed for oracle/_ref):
     python tests/golden/gen_full_scale.py            # both scenes
     python tests/golden/gen_full_scale.py --scene elf
-Outputs tests/golden/{lucy,elf,spheres}_full_tiles.npz.  lucy takes ~10 min of 8 cores (28.05 M
-triangle parse + reference BVH build dominate), elf ~5 min.
+Outputs tests/golden/{bunny,lucy,elf,spheres}_full_tiles.npz.  lucy takes ~10 min of 8 cores (28.05 M
+triangle parse + reference BVH build dominate), elf ~5 min, bunny ~5 min (the per-tile timing).
 """
 from __future__ import annotations
 
@@ -44,6 +49,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 # BASELINE.json configs: scene writer kwargs, frame, spp, integrator (SP_INTEGRATOR_*), picks
 CONFIGS = {
+    # configs[2], the north-star frame: four bunnies (clearcoat, lambertian, glossy) on a glossy plane
+    "bunny": dict(writer="write_bunny_scene", kw={}, file="bunny.sp", mesh="ply_files/bunny/reconstruction/bun_zipper.ply",
+                  w=1920, h=1080, spp=256, integrator=6, probe_step=5, picks=(8, 8, 8), seed=6, slow=8, slow_spp=16),
     "lucy": dict(writer="write_lucy_scene", kw=dict(n=1529), file="lucy.sp", mesh="ply_files/lucy_1529.ply",
                  w=1920, h=1080, spp=256, integrator=6, probe_step=5, picks=(12, 10, 10), seed=3),
     "elf": dict(writer="write_elf_scene", kw=dict(n=290, max_depth=16), file="elf.sp",
@@ -158,6 +166,46 @@ def pick_tiles(probe: np.ndarray, ids: np.ndarray, env, w: int, h: int, picks, s
     return np.array(chosen, dtype=np.int32), np.array(kinds)
 
 
+def _time_tiles_worker(job):
+    """One worker process: each tile of `ids` rendered alone on one thread, wall time per tile."""
+    path, w, h, integ, spp, ids = job
+    L = ref_lib()
+    sc = L.ref_scene_create(path.encode(), w, h)
+    assert sc, L.ref_last_error()
+    out = np.zeros((1, 64, 3), dtype=np.float32)
+    t = np.zeros(len(ids))
+    for k, tile in enumerate(ids):
+        one = np.array([tile], dtype=np.int32)
+        best = float("inf")
+        for _ in range(2):  # the smaller of two runs: a tile's cost, not a scheduling hiccup
+            t0 = time.perf_counter()
+            rc = L.ref_render_tiles(sc, integ, spp, one.ctypes.data_as(C.POINTER(C.c_int32)), 1, 1,
+                                    out.ctypes.data_as(C.POINTER(C.c_float)))
+            best = min(best, time.perf_counter() - t0)
+            assert rc == 0
+        t[k] = best
+    L.ref_scene_free(sc)
+    return t
+
+
+def slowest_tiles(path, w, h, integ, spp, n_pick, exclude, procs):
+    """The n_pick slowest whole tiles of the frame on the reference (one thread per tile)."""
+    import multiprocessing as mp
+    import simplepath_amd as sp
+    n = sp.TileScheduler(w, h).get_num_tiles()
+    ids = np.arange(n, dtype=np.int32)
+    parts = [ids[k::procs] for k in range(procs)]
+    with mp.get_context("fork").Pool(procs) as pool:
+        times = pool.map(_time_tiles_worker, [(path, w, h, integ, spp, p) for p in parts])
+    t = np.zeros(n)
+    for p, tp in zip(parts, times):
+        t[p] = tp
+    full = np.array([inside_mask(int(i), w, h).all() for i in ids])
+    order = [int(i) for i in np.argsort(-t, kind="stable") if full[i] and int(i) not in exclude]
+    picked = np.array(order[:n_pick], dtype=np.int32)
+    return picked, t[picked], float(np.mean(t))
+
+
 def generate(name: str, workdir: str, threads: int) -> str:
     import simplepath_amd as sp
     from simplepath_amd import scenes
@@ -199,8 +247,19 @@ def generate(name: str, workdir: str, threads: int) -> str:
         env_probe = render(L, sc0, integ, 1, probe_ids, threads)
         L.ref_scene_free(sc0)
     else:
-        env = np.array({"lucy": [1.0, 1.0, 1.3], "elf": [0.75, 0.75, 0.75]}[name], dtype=np.float32)
+        # an escaped camera ray sees the environment light's radiance (bunny.sp has none: 0)
+        env = np.array({"lucy": [1.0, 1.0, 1.3], "elf": [0.75, 0.75, 0.75], "bunny": [0.0, 0.0, 0.0]}[name],
+                       dtype=np.float32)
     ids, kinds = pick_tiles(probe, probe_ids, env, w, h, cfg["picks"], cfg["seed"], env_probe)
+    extra = {}
+    if cfg.get("slow"):
+        slow, slow_t, mean_t = slowest_tiles(path, w, h, integ, cfg["slow_spp"], cfg["slow"], set(ids.tolist()),
+                                             max(1, threads))
+        ids = np.concatenate([ids, slow]).astype(np.int32)
+        kinds = np.concatenate([kinds, np.array(["slowest"] * slow.size)])
+        extra = dict(slow_tile_s=slow_t, mean_tile_s=mean_t, slow_spp=cfg["slow_spp"])
+        print(f"[{name}] slowest tiles {slow.tolist()} ({slow_t.min() / mean_t:.1f}-{slow_t.max() / mean_t:.1f}x "
+              f"the mean at {cfg['slow_spp']} spp, {time.time() - t0:.0f} s)", flush=True)
     t1 = time.time()
     out = render(L, sc, integ, spp, ids, threads)
     print(f"[{name}] {ids.size} tiles at {spp} spp ({time.time() - t1:.0f} s)", flush=True)
@@ -213,20 +272,20 @@ def generate(name: str, workdir: str, threads: int) -> str:
                         bvh_ref=json.dumps(depth_ref), bvh_sah=json.dumps(depth_sah),
                         rsqrt_entries=rs["entries"], rsqrt_bits=rs["bits"], rsqrt_zero=rs["zero_result"],
                         rsqrt_denorm=rs["denorm_result"], host_cpu=host_cpu(),
-                        generator="tests/golden/gen_full_scale.py (oracle/_ref = reference sources)")
+                        generator="tests/golden/gen_full_scale.py (oracle/_ref = reference sources)", **extra)
     print(f"[{name}] wrote {dst} ({time.time() - t0:.0f} s total)", flush=True)
     return dst
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scene", choices=["lucy", "elf", "spheres", "all"], default="all")
+    ap.add_argument("--scene", choices=["bunny", "lucy", "elf", "spheres", "all"], default="all")
     ap.add_argument("--workdir", default=os.path.join("/tmp", "sp_full_scale"))
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     a = ap.parse_args()
     if not os.path.exists(REF_LIB):
         sys.exit("oracle/_ref/libsp_ref.so is missing: run oracle/build_ref.sh (needs /root/reference)")
-    for name in (["spheres", "elf", "lucy"] if a.scene == "all" else [a.scene]):
+    for name in (["bunny", "spheres", "elf", "lucy"] if a.scene == "all" else [a.scene]):
         generate(name, a.workdir, a.threads)
 
 

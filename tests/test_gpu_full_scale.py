@@ -1,7 +1,11 @@
-"""Full-scale parity for BASELINE.json configs[3] and configs[4]: the HIP path against the
+"""Full-scale parity for BASELINE.json configs[1]-[4]: the HIP path against the
 reference's own output on a fixed tile subset of the FULL scenes (tests/golden/
 gen_full_scale.py renders them with oracle/_ref = the reference's sources).
 
+  * bunny.sp (configs[2], the north-star frame): 1920x1080 @ 256 spp, DirectLighting -- 32 tiles
+    (silhouettes, high-contrast, random, and the 8 slowest tiles of the frame timed on the
+    reference), through the 1-GPU megakernel with its tile-order probe and the 8-way shard's
+    sample chunks;
   * lucy.sp: 28.05 M-triangle PLY stand-in, 1920x1080 @ 256 spp, DirectLighting -- 32 tiles
     (silhouettes, high-contrast drapery / floor contact, random);
   * elf.sp: 1.0 M-triangle binary STL stand-in, 4096x4096 @ 1024 spp, IterativeRRNEE with
@@ -174,3 +178,67 @@ def test_full_scale_lucy_sah_megakernel():
     print(f"lucy SAH megakernel: rel_l2={r:.3e}, bit-exact pixels {frac:.5f}")
     assert r < REL_L2_TOL
     assert frac >= 0.999
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("bvh", [1, 0])
+def test_full_scale_bunny_frame(bvh):
+    # configs[2], the north-star frame (bunny.sp 1920x1080 @ 256 spp, DirectLighting; main.cpp:77-107),
+    # rendered WHOLE exactly as the 1-GPU bench renders it (AUTO: the megakernel with its tile-order
+    # probe -- 32400 tiles, ~8 per persistent wave), then compared with the reference's own tiles:
+    # silhouettes, high-contrast, random, and the 8 slowest tiles of the frame (the bunnies against
+    # the glossy floor)
+    g, s = full_scene("bunny")
+    s.upload(device=0, bvh_mode=bvh)
+    built = json.loads(str(g["bvh_ref" if bvh == 1 else "bvh_sah"]))
+    info = s.bvh_info()
+    assert (info["depth"], info["nodes"], info["slots"]) == (built["depth"], built["nodes"], built["slots"])
+    ids = g["tile_ids"].astype(np.int32)
+    assert (g["kinds"] == "slowest").sum() == 8
+    ref = g["radiance"]
+    frame, st = sp.render_tiles(s, "direct_lighting", int(g["spp"]))
+    assert frame.shape[0] == 32400
+    assert st.pipeline == sp.PIPELINES["megakernel"] and st.launches == 3  # probe, partition, render
+    assert st.stack_depth == expected_stack(built, bvh)
+    out = frame[ids]
+    r = rel_l2(out, ref)
+    frac = float(np.mean(np.all(out == ref, axis=-1)))
+    print(f"bunny bvh={bvh} whole frame: rel_l2={r:.3e}, bit-exact pixels {frac:.5f}")
+    if bvh == 1:
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), (r, frac)
+    else:
+        assert r < REL_L2_TOL and frac >= 0.999
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("bvh", [1, 0])
+def test_full_scale_bunny_shard_chunks(bvh):
+    # the pipeline of the 2-8-GPU shards: each rank's whole shard of an 8-way split
+    # (ColumnMajorTileScheduler.shard, 4050 tiles; AUTO: the sample chunks below 24000 tiles),
+    # compared with the reference on the golden tiles that shard holds
+    from simplepath_amd import shard
+    g, s = full_scene("bunny")
+    s.upload(device=0, bvh_mode=bvh)
+    ids = g["tile_ids"].astype(np.int32)
+    ref = g["radiance"]
+    n_tiles = sp.TileScheduler(int(g["width"]), int(g["height"])).get_num_tiles()
+    out = np.zeros_like(ref)
+    covered = np.zeros(ids.size, dtype=bool)
+    for rank in range(8):
+        mine = shard.shard_tiles(n_tiles, rank, 8)
+        pos = {int(t): k for k, t in enumerate(mine)}
+        sel = np.array([k for k, t in enumerate(ids) if int(t) in pos], dtype=np.int64)
+        if sel.size == 0:
+            continue
+        o, st = sp.render_tiles(s, "direct_lighting", int(g["spp"]), mine)
+        assert st.pipeline == sp.PIPELINES["chunks"] and o.shape[0] == mine.size
+        out[sel] = o[[pos[int(ids[k])] for k in sel]]
+        covered[sel] = True
+    assert covered.all()
+    r = rel_l2(out, ref)
+    frac = float(np.mean(np.all(out == ref, axis=-1)))
+    print(f"bunny bvh={bvh} 8-way shard chunks: rel_l2={r:.3e}, bit-exact pixels {frac:.5f}")
+    if bvh == 1:
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), (r, frac)
+    else:
+        assert r < REL_L2_TOL and frac >= 0.999
