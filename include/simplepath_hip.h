@@ -224,8 +224,11 @@ enum {
                                    ballot/prefix-sum shadow-ray compaction (sp_wave.hip)         */
     SP_PIPELINE_SAMPLE_CHUNKS = 3, /* DirectLighting: each pixel's samples in parallel chunks
                                       (stream state snapshots; sp_chunk.hip)                      */
-    SP_RENDER_STAGE_TIMING = 4  /* flag: HIP events between launches fill sp_render_stats.stage_ms
+    SP_RENDER_STAGE_TIMING = 4, /* flag: HIP events between launches fill sp_render_stats.stage_ms
                                    (waits for the render)                                          */
+    SP_RENDER_PER_LANE_QUERIES = 8 /* flag (ABI 5): IterativeRRNEE walks each ray on its own lane
+                                   instead of dealing a bounce's MIS and next closest-hit walks
+                                   over the wave (identical images; the comparison path)           */
 };
 
 /* Accelerator options of sp_scene_upload_ex (ABI 4).  Zero-initialise: 0 = automatic. */

@@ -185,11 +185,12 @@ class ColumnMajorTileScheduler(TileScheduler):
 
 PIPELINES = {"auto": 0, "megakernel": 1, "wavefront": 2, "chunks": 3}
 STAGE_TIMING = 4  # SP_RENDER_STAGE_TIMING
+PER_LANE_QUERIES = 8  # SP_RENDER_PER_LANE_QUERIES (ABI 5)
 
 
 def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeline="auto",
             stage_timing=False, waves_per_simd=0, chunks_per_pixel=0, chunk_max_gb=0.0,
-            tile_order_factor=0.0) -> tuple:
+            tile_order_factor=0.0, per_lane_queries=False) -> tuple:
     if isinstance(integrator, str):
         integrator = string_to_integrator_type(integrator)
     p = _abi.sp_render_params()
@@ -201,7 +202,8 @@ def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeli
         p.tile_ids = keep.ctypes.data_as(C.POINTER(C.c_int32))
         p.num_tiles = keep.size
     p.stream = stream
-    p.flags = (PIPELINES[pipeline] if isinstance(pipeline, str) else int(pipeline)) | (STAGE_TIMING if stage_timing else 0)
+    p.flags = ((PIPELINES[pipeline] if isinstance(pipeline, str) else int(pipeline)) | (STAGE_TIMING if stage_timing else 0)
+               | (PER_LANE_QUERIES if per_lane_queries else 0))
     p.waves_per_simd = int(waves_per_simd)
     p.chunks_per_pixel = int(chunks_per_pixel)
     p.chunk_max_gb = float(chunk_max_gb)
@@ -218,7 +220,8 @@ def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Opt
                  pipeline="auto", **options):
     """Render tiles on the GPU; returns (tile-packed radiance [n,64,3] float32, RenderStats).
     options: waves_per_simd, chunks_per_pixel, chunk_max_gb (sp_render_params, ABI 4),
-    tile_order_factor (ABI 5: 0 automatic, > 0 forced with that factor, < 0 queue order)."""
+    tile_order_factor (ABI 5: 0 automatic, > 0 forced with that factor, < 0 queue order),
+    per_lane_queries (ABI 5: IterativeRRNEE without the merged query pass -- the comparison path)."""
     p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids),
                       pipeline=pipeline, **options)
     n = keep.size if keep is not None else TileScheduler(scene.width, scene.height).get_num_tiles()

@@ -866,6 +866,7 @@ static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params
     d.wide_closest = (opts.wide_closest && !wide.words.empty()) ? 1 : 0;
     d.stack_depth  = stack_entries(bvh.max_depth, wide.depth, lbvh.max_depth, d.wide_closest != 0);
     d.stackless   = stackless ? 1 : 0;
+    d.merge_queries = 1; // per render: SP_RENDER_PER_LANE_QUERIES clears it
     d.parents       = nullptr;
     d.light_parents = nullptr;
     if (d.stackless) { // deeper than the LDS budget: parent links instead of a stack
@@ -973,7 +974,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     if (p->chunks_per_pixel < 0) return fail(SP_ERR_ARG, "chunks_per_pixel < 0");
     if (!(p->chunk_max_gb >= 0.0f)) return fail(SP_ERR_ARG, "chunk_max_gb < 0");
     if (p->tile_order_factor != p->tile_order_factor) return fail(SP_ERR_ARG, "tile_order_factor is NaN");
-    if ((p->flags & ~(3 | SP_RENDER_STAGE_TIMING)) != 0) return fail(SP_ERR_ARG, "unknown flags");
+    if ((p->flags & ~(3 | SP_RENDER_STAGE_TIMING | SP_RENDER_PER_LANE_QUERIES)) != 0) return fail(SP_ERR_ARG, "unknown flags");
     SP_HIP(hipSetDevice(s->device));
     int32_t integ = p->integrator;
     if (integ == SP_INTEGRATOR_NOT_SPECIFIED) integ = s->host->integrator;
@@ -1274,6 +1275,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             s->mt_waves = waves;
         }
         SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
+        spd::Scene sc_run    = s->dev; // the resident scene with this render's options
+        sc_run.merge_queries = (p->flags & SP_RENDER_PER_LANE_QUERIES) ? 0 : 1;
         spd::RenderArgs a{};
         a.out          = d_out;
         a.tile_ids     = d_ids;
@@ -1341,7 +1344,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             pr.tile_time = s->d_tile_time;
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
-            SP_HIP(spd::launch_probe(s->dev, pr, integ, variant, blocks, lds_bytes, stream));
+            SP_HIP(spd::launch_probe(sc_run, pr, integ, variant, blocks, lds_bytes, stream));
             SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, s->d_order, stream));
             SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
             a.order = s->d_order;
@@ -1351,7 +1354,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             if (!s->ev_render) SP_HIP(hipEventCreate(&s->ev_render));
             SP_HIP(hipEventRecord(s->ev_render, stream));
         }
-        SP_HIP(spd::launch_render(s->dev, a, integ, variant, blocks, lds_bytes, stream));
+        SP_HIP(spd::launch_render(sc_run, a, integ, variant, blocks, lds_bytes, stream));
         if (tdiag) { // diagnostic: waits for the render
             SP_HIP(hipStreamSynchronize(stream));
             std::vector<unsigned long long> rec((size_t)n_tiles * 8);

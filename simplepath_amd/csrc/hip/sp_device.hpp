@@ -119,6 +119,10 @@ struct Scene {
     // BVHs too deep for the LDS stack budget: binary walks climb parent links instead of popping
     // a stack (same visiting order and box tests; sp_path.hpp bvh_next)
     int             stackless;
+    // IterativeRRNEE: a bounce's MIS-ray and next closest-hit BVH walks dealt over the wave
+    // (sp_path.hpp mq_run; needs wide_closest and the stack).  Set per render: 1 unless
+    // SP_RENDER_PER_LANE_QUERIES asks for the per-lane walks (the comparison).
+    int             merge_queries;
     const uint32_t* parents;       // parent of each geometry node (root: itself)
     const uint32_t* light_parents; // parent of each light-BVH node
 };

@@ -25,8 +25,10 @@ using namespace spm;
 // region's share of wave time and its lane occupancy come out separately.  Regions:
 // 0 = a whole sample (integrate), 1 = the 16-sample glossy rho estimate, 2 = closest-hit queries
 // (camera / extension rays: their entry occupancy is the fraction of paths alive), 3 = shadow and
-// MIS-ray queries; the block-served IterativeRRNEE kernel adds 4 = advancing lanes between rounds,
-// 5 = waiting at the post barrier, 6 = serving estimates, 7 = waiting at the result barrier.  Written by the first active lane into a per-wave LDS row,
+// MIS-ray queries; IterativeRRNEE's merged query pass (mq_run) adds 5 = the whole pass and 4 = its
+// walk steps, timed per loop iteration, so 4's occupancy is that of the lanes still walking;
+// 6 / 7 = the steps of every 8-wide closest-hit / any-hit walk (per iteration, like 4).
+// Written by the first active lane into a per-wave LDS row,
 // flushed to the render's tile_diag buffer at kernel end (sp_mega.hpp).
 #ifdef SP_WAVE_PROF
 static __shared__ unsigned long long wprof_lds[16 * 16];
@@ -718,14 +720,21 @@ __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float 
     int            sp  = 0;
     uint32_t       node = 0;
     while (true) {
+#ifdef SP_WAVE_PROF
+        const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 7: any-hit walk steps
+#define SP_WPROF_ANY wprof_end(7, t_it)
+#else
+#define SP_WPROF_ANY
+#endif
         const WideHits wh = wide_visit(sc, node, ray, inv, tmin, tmax);
         for (uint32_t m = wh.leaf; m; m &= m - 1) {
             const int      k    = __ffs(m) - 1;
             const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
             const uint32_t base = wh.leaf_base + (meta & 31u);
             for (uint32_t j = 0; j < (meta >> 5); ++j)
-                if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) return true;
+                if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) { SP_WPROF_ANY; return true; }
         }
+        SP_WPROF_ANY;
         if (wh.inner) {
             const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o); // octant order
             if (rest) {
@@ -771,6 +780,9 @@ __device__ __forceinline__ Hit wide_closest(const Scene& sc, const Ray& ray, flo
     int            sp   = 0;
     uint32_t       node = 0;
     while (true) {
+#ifdef SP_WAVE_PROF
+        const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 6: closest-hit walk steps
+#endif
         const WideHits wh = wide_visit(sc, node, ray, inv, tmin, h.t);
         for (uint32_t m = wh.leaf; m; m &= m - 1) {
             const int      k    = __ffs(m) - 1;
@@ -778,6 +790,9 @@ __device__ __forceinline__ Hit wide_closest(const Scene& sc, const Ray& ray, flo
             const uint32_t base = wh.leaf_base + (meta & 31u);
             for (uint32_t j = 0; j < (meta >> 5); ++j) prim_closest(sc, base + j, ray, tmin, h, sc.wslot_tri);
         }
+#ifdef SP_WAVE_PROF
+        wprof_end(6, t_it);
+#endif
         if (wh.inner) {
             const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o);
             if (rest) {
@@ -898,8 +913,8 @@ __device__ __forceinline__ Hit bvh_closest(const Scene& sc, const Ray& ray, floa
     return h;
 }
 
-// Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH}
-__device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+// Scene::intersect (base/Scene.h:74): ListAccelerator{unbounded..., BVH} -- the unbounded shapes
+__device__ __forceinline__ Hit scene_intersect_unbounded(const Scene& sc, const Ray& ray, float tmin, float tmax)
 {
     Hit h;
     h.t    = tmax;
@@ -911,6 +926,11 @@ __device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, 
         const bool  hit = (s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
         if (hit) { h.t = t; h.code = ((uint32_t)s.kind << CODE_SHIFT) | (uint32_t)sid; }
     }
+    return h;
+}
+__device__ __forceinline__ Hit scene_intersect(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    Hit h = scene_intersect_unbounded(sc, ray, tmin, tmax);
     if (sc.n_nodes == 0) return h;
     if (sc.wide_closest) return wide_closest(sc, ray, tmin, h, st);
     return sc.stackless ? bvh_closest<true>(sc, ray, tmin, h, st) : bvh_closest<false>(sc, ray, tmin, h, st);
@@ -946,14 +966,19 @@ __device__ __forceinline__ bool bvh_any(const Scene& sc, const Ray& ray, float t
     return false;
 }
 
-// any-hit over the geometry accelerator (ListAccelerator::intersect_p_impl)
-__device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+// any-hit over the geometry accelerator (ListAccelerator::intersect_p_impl): the unbounded shapes
+__device__ __forceinline__ bool unbounded_any(const Scene& sc, const Ray& ray, float tmin, float tmax)
 {
     for (int i = 0; i < sc.n_unbounded; ++i) {
         const UShape s = uload_shape(sc.shapes + uload_u32(sc.unbounded + i));
         float        t;
         if ((s.kind == SP_PRIM_SPHERE) ? sphere_t(s.w2o, ray, tmin, tmax, t) : plane_t(s.w2o, ray, tmin, tmax, t)) return true;
     }
+    return false;
+}
+__device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    if (unbounded_any(sc, ray, tmin, tmax)) return true;
     if (sc.n_nodes == 0) return false;
     if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
     return sc.stackless ? bvh_any<true>(sc, ray, tmin, tmax, st) : bvh_any<false>(sc, ray, tmin, tmax, st);
@@ -1635,9 +1660,32 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
 }
 
 #if SP_SERVE_RHO
-// [wave][call site k][weight][owner lane]: weights served to the owners (serve_rho)
-static __shared__ float   srv_w[4][4][2][64];
-static __shared__ uint8_t srv_req[4][4 * 64]; // request r: owner lane | k << 6 (k = 3: the bounce's sample)
+// Per-wave LDS of the IterativeRRNEE megakernel, used by two phases of a bounce in turn:
+//   serve_rho: srv_w [call site k][weight][owner lane] (weights served to the owners, 512 words)
+//              and srv_req (request r: owner lane | k << 6, k = 3: the bounce's sample; 256 bytes);
+//   the merged query pass (mq_run, after every served weight has been taken): the posted rays
+//              and their results, MQ_* below.
+#ifndef SP_MERGE_QUERIES
+#define SP_MERGE_QUERIES 1
+#endif
+enum : int {
+    MQ_O = 0,      // shared origin of an owner's two rays (x, y, z planes of 64)
+    MQ_D3 = 192,   // MIS ray direction (estimate_direct_mis, Integrator.cpp:527-533)
+    MQ_T3 = 384,   // its t_min
+    MQ_D1 = 448,   // next bounce's direction (Integrator.cpp:570); result {t, code, beta} overwrites it
+    MQ_T1 = 640,   // its t_min; result gamma overwrites it
+    MQ_H1T = 704,  // its t_max after the light and unbounded-shape tests (the walk's starting hit)
+    MQ_H1C = 768,  // the starting hit's primitive code
+    MQ_R3 = 832,   // MIS ray's geometry any-hit result
+    MQ_Q = 896,    // queue: 128 bytes, query r = owner lane | any-hit << 7
+    MQ_CNT = 928,  // next unclaimed query
+    MQ_WORDS = 929,
+    SRV_W = 0, SRV_REQ = 512, SRV_WORDS = 576,
+    SRV_WAVE_WORDS = (SP_MERGE_QUERIES && MQ_WORDS > SRV_WORDS) ? MQ_WORDS : SRV_WORDS
+};
+static __shared__ uint32_t srv_lds[4][SRV_WAVE_WORDS];
+__device__ __forceinline__ float*   srv_w_at(int wave, int k, int j) { return reinterpret_cast<float*>(&srv_lds[wave][SRV_W + (k * 2 + j) * 64]); }
+__device__ __forceinline__ uint8_t* srv_req_of(int wave) { return reinterpret_cast<uint8_t*>(&srv_lds[wave][SRV_REQ]); }
 #endif
 
 // OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
@@ -1653,8 +1701,8 @@ __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rn
         else if (rng.srv_B) k = (d == 0u) ? 0 : (d == rng.srv_dc) ? 1 : (d == 2u * rng.srv_dc + rng.srv_coat) ? 2 : -1;
         if (k >= 0) {
             const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-            w[0]           = srv_w[wave][k][0][lane];
-            w[1]           = srv_w[wave][k][1][lane];
+            w[0]           = srv_w_at(wave, k, 0)[lane];
+            w[1]           = srv_w_at(wave, k, 1)[lane];
             rng_skip_reserved(rng, (int)rng.srv_dc);
             return;
         }
@@ -2272,7 +2320,7 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
         if (want) {
             rng_reserve(c.rng, (int)(3u * dc + coat));
             pw = ((uint32_t)c.rng.cur << 16) | (uint32_t)c.rng.idx;
-            for (int k = 0; k < 3; ++k) srv_req[wave][r++] = (uint8_t)(lane | (k << 6));
+            for (int k = 0; k < 3; ++k) srv_req_of(wave)[r++] = (uint8_t)(lane | (k << 6));
             c.rng.srv_on   = 1;
             c.rng.srv_B    = true;
             c.rng.srv_pos  = c.rng.draws;
@@ -2281,7 +2329,7 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
         }
         if (want_a) {
             pwa                 = c.rng.srv_pwA;
-            srv_req[wave][r++] = (uint8_t)(lane | (3 << 6));
+            srv_req_of(wave)[r++] = (uint8_t)(lane | (3 << 6));
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2295,7 +2343,7 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
     const int      nact = __popcll(act);
     for (int r0 = 0; r0 < total; r0 += nact) {
         const int      r = r0 + rank;
-        const uint32_t e = (r < total) ? (uint32_t)srv_req[wave][r] : 0u;
+        const uint32_t e = (r < total) ? (uint32_t)srv_req_of(wave)[r] : 0u;
         const int      o = (int)(e & 63u), k = (int)(e >> 6);
         // the owner's inputs (all lanes take part in the exchange)
         const f3       owo   = mk(__shfl(wl.x, o, 64), __shfl(wl.y, o, 64), __shfl(wl.z, o, 64));
@@ -2314,14 +2362,200 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
             }
             float w[2];
             served_weights(c.sc.materials[obase], owo, c.rng.base - lane + o, cur, idx, c.q, w);
-            srv_w[wave][k][0][o] = w[0];
-            srv_w[wave][k][1][o] = w[1];
+            srv_w_at(wave, k, 0)[o] = w[0];
+            srv_w_at(wave, k, 1)[o] = w[1];
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+#if SP_MERGE_QUERIES
+// ---------------------------------------------------------------- merged query pass
+// Once a bounce's served estimates are taken, a live lane holds two ray queries that depend on
+// nothing else still to come: the MIS ray of its (last) light's estimate_direct_mis
+// (Integrator.cpp:527-533: intersect_lights, then intersect_p) and the next bounce's closest hit
+// (:558-563, direction fixed at :570).  In lock step each was a wave-wide walk whose length is
+// its slowest lane's, at the occupancy of the paths still alive (0.59-0.67).  Here the cheap
+// parts stay with the owner (the light tests and the unbounded shapes), and the BVH walks are
+// posted to LDS (rays, starting hits) and dealt over every lane of the wave -- ended paths
+// included: a lane walks one query, writes its result for the owner and claims the next
+// unclaimed one, so the pass takes about (total walk steps) / 64 plus one walk, not the sum of
+// two slowest walks.  Each query is the walk the owner would have run itself: any-hit queries
+// visit nodes in wide_any's order, closest-hit ones in wide_closest's (an any-hit query's
+// t_max is FLT_MAX, so wide_closest's distance culling never drops a group for it), with the
+// same box and primitive tests.  Results, ray counts and stream words are unchanged.
+__device__ __forceinline__ float    mq_f(const uint32_t* m, int i) { return __uint_as_float(m[i]); }
+__device__ __forceinline__ f3       mq_f3(const uint32_t* m, int b, int o) { return mk(mq_f(m, b + o), mq_f(m, b + 64 + o), mq_f(m, b + 128 + o)); }
+__device__ __forceinline__ void     mq_put3(uint32_t* m, int b, int o, f3 v)
+{
+    m[b + o]       = __float_as_uint(v.x);
+    m[b + 64 + o]  = __float_as_uint(v.y);
+    m[b + 128 + o] = __float_as_uint(v.z);
+}
+__device__ __forceinline__ void mq_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// All lanes in integrate() call it; total = queries in m[MQ_Q..] (posted and synchronised by the caller).
+__device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, int total)
+{
+    const int      lane = threadIdx.x & 63;
+    const uint64_t act  = __ballot(1);
+    int            q    = __popcll(act & ((1ull << lane) - 1ull)); // first round: one query per lane present
+    if (q == 0) m[MQ_CNT] = (uint32_t)__popcll(act);
+    mq_sync();
+    const int      half = st.depth >> 1;
+    const uint8_t* qs   = reinterpret_cast<const uint8_t*>(m + MQ_Q);
+    Ray            ray;
+    f3             inv  = mk(0, 0, 0);
+    uint32_t       o    = 0, node = 0;
+    float          tmin = 0.0f;
+    Hit            h;
+    bool           any  = false;
+    int            own  = 0, sp = 0;
+    auto start = [&](int qi) {
+        const uint32_t e = qs[qi];
+        own  = (int)(e & 63u);
+        any  = (e & 0x80u) != 0u;
+        ray.o = mq_f3(m, MQ_O, own);
+        ray.d = mq_f3(m, any ? MQ_D3 : MQ_D1, own);
+        tmin  = mq_f(m, (any ? MQ_T3 : MQ_T1) + own);
+        h.t    = any ? k_infinite : mq_f(m, MQ_H1T + own);
+        h.code = any ? 0xffffffffu : m[MQ_H1C + own];
+        h.beta = h.gamma = 0.0f;
+        inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+        o    = dir_sign_bits(ray.d);
+        sp   = 0;
+        node = 0;
+    };
+    bool have = q < total;
+    if (have) start(q);
+    while (have) {
+#ifdef SP_WAVE_PROF
+        const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 4: lanes walking, per step
+#endif
+        const WideHits wh    = wide_visit(sc, node, ray, inv, tmin, h.t);
+        bool           found = false;
+        for (uint32_t mm = wh.leaf; mm && !found; mm &= mm - 1) {
+            const int      k    = __ffs(mm) - 1;
+            const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
+            const uint32_t base = wh.leaf_base + (meta & 31u);
+            for (uint32_t j = 0; j < (meta >> 5); ++j) {
+                if (any) {
+                    if (prim_any(sc, base + j, ray, tmin, h.t, sc.wslot_tri)) { found = true; break; }
+                } else {
+                    prim_closest(sc, base + j, ray, tmin, h, sc.wslot_tri);
+                }
+            }
+        }
+        bool end = found;
+        if (!found) {
+            if (wh.inner) {
+                const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o); // octant order
+                if (rest) {
+                    st.s[sp * 64 + st.lane]          = (wh.child_base << 8) | rest;
+                    st.s[(sp + half) * 64 + st.lane] = __float_as_uint(wh.t_rest);
+                    ++sp;
+                }
+                node = wh.child_base + (uint32_t)wh.nearest;
+            } else {
+                end = true;
+                while (sp > 0) {
+                    const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
+                    if (__uint_as_float(st.s[(sp - 1 + half) * 64 + st.lane]) > h.t) { --sp; continue; }
+                    uint32_t  mk8 = e & 0xffu;
+                    const int k   = __ffs(mk8) - 1;
+                    mk8 &= mk8 - 1;
+                    if (mk8) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | mk8;
+                    else --sp;
+                    node = (e >> 8) + ((uint32_t)k ^ o);
+                    end  = false;
+                    break;
+                }
+            }
+        }
+        if (end) {
+            if (any) {
+                m[MQ_R3 + own] = found ? 1u : 0u;
+            } else { // {t, code, beta} over the direction, gamma over t_min: read by this lane only
+                m[MQ_D1 + own]       = __float_as_uint(h.t);
+                m[MQ_D1 + 64 + own]  = h.code;
+                m[MQ_D1 + 128 + own] = __float_as_uint(h.beta);
+                m[MQ_T1 + own]       = __float_as_uint(h.gamma);
+            }
+            q    = (int)atomicAdd(&m[MQ_CNT], 1u);
+            have = q < total;
+            if (have) start(q);
+        }
+#ifdef SP_WAVE_PROF
+        wprof_end(4, t_it);
+#endif
+    }
+    mq_sync();
+}
+
+// mis_material_part (estimate_direct_mis after its shadow ray, Integrator.cpp:505-535) with the MIS
+// ray's occlusion test left to the merged pass: true when its BVH walk was posted (origin,
+// direction, t_min in the owner's MQ_O / MQ_D3 / MQ_T3 slots).  e_occ is the estimate if that ray
+// is occluded, e_vis if not (the MIS term is a pure function of values known now, computed with
+// the same operations in the same order); otherwise the estimate is final in e_occ.  Counts and
+// draws are mis_material_part's.
+__device__ __forceinline__ bool mis_material_part_mq(Ctx& c, const Light& l, const LSample& ls, f3 p, f3 n, f3 wo, int mid,
+                                                     uint32_t* m, rgb& e_occ, rgb& e_vis)
+{
+    const int lane = threadIdx.x & 63;
+    rgb       Lr   = mkc(0, 0, 0);
+    const f3  wi   = ls.ray.d;
+    const rgb be   = material_eval(c.sc, mid, wo, wi, n, c.rng, c.q);
+    if (!cblack(be)) {
+        const float bp = material_pdf(c.sc, mid, wo, wi, n, c.rng, c.q);
+        if (bp > 0.0f) {
+            const float w = balance(ls.pdf, ls.pdf + bp);
+            Lr            = cadd(Lr, cscale(cmul(be, ls.L), abs_f(dot(wi, n)) * w / ls.pdf));
+        }
+    }
+    e_occ            = Lr;
+    const MSample ms = material_sample(c.sc, mid, wo, n, c.rng, c.q);
+    if (ms.pdf == 0.0f || cblack(ms.color)) return false;
+    const float lp = light_pdf(c.sc, l, p, ms.dir);
+    if (lp == 0.0f) return false;
+    const float w = balance(ms.pdf, ms.pdf + lp);
+    Ray         mr;
+    mr.o             = p;
+    mr.d             = ms.dir;
+    const float mmin = ray_offset(n, ms.dir);
+    ++c.rays;
+    LightHit lh;
+    SP_WPROF(3, lh = scene_intersect_lights(c.sc, mr, mmin, k_infinite, c.st));
+    if (!lh.hit) return false;
+    ++c.shadow; // occluded(): Scene::intersect_p = geometry (unbounded shapes, BVH) || lights
+    ++c.rays;
+    if (unbounded_any(c.sc, mr, mmin, k_infinite)) return false; // occluded
+    e_vis = cadd(Lr, cdivs(cscale(cscale(cmul(ms.color, light_hit_L(c.sc, lh, mr.d, c.q)), abs_f(dot(ms.dir, n))), w), ms.pdf));
+    if (c.sc.n_nodes == 0) {
+        if (!lights_any(c.sc, mr, mmin, k_infinite, c.st)) e_occ = e_vis;
+        return false;
+    }
+    mq_put3(m, MQ_O, lane, p);
+    mq_put3(m, MQ_D3, lane, ms.dir);
+    m[MQ_T3 + lane] = __float_as_uint(mmin);
+    return true;
+}
+// after mq_run: the MIS ray's Scene::intersect_p = the BVH walk's result || the lights
+__device__ __forceinline__ bool mis_ray_occluded(Ctx& c, const uint32_t* m)
+{
+    const int lane = threadIdx.x & 63;
+    if (m[MQ_R3 + lane] != 0u) return true;
+    Ray mr;
+    mr.o = mq_f3(m, MQ_O, lane);
+    mr.d = mq_f3(m, MQ_D3, lane);
+    return lights_any(c.sc, mr, mq_f(m, MQ_T3 + lane), k_infinite, c.st);
+}
+#endif
 
 // IntegratorIterativeRRNEE (Integrators/Integrator.cpp:550) with wave-served estimates: the same
 // per-lane operations as the form below, but a lane whose path has ended stays in the loop (no
@@ -2333,15 +2567,29 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
     float tmin = k_ray_epsilon, tmax = k_infinite;
     constexpr float rr_cut = 0.1f;
     bool  alive = true;
+    Query qr;
+#if SP_MERGE_QUERIES
+    // merged query pass (mq_run) on scenes whose closest hits walk the 8-wide BVH with the LDS
+    // stack (SAH uploads); the reference-order BVH and stackless walks keep the per-lane queries
+    const bool mq     = c.sc.merge_queries != 0 && c.sc.wide_closest != 0 && !c.sc.stackless;
+    uint32_t*  m      = srv_lds[threadIdx.x >> 6];
+    bool       traced = false; // this bounce's closest hit came from the previous merged pass
+#endif
     for (int depth = 0; depth < c.sc.max_depth; ++depth) {
         if (!__any(alive)) break;
-        Query   qr;
         MSample s;
         f3      wo  = mk(0, 0, 0), n = mk(0, 0, 0);
         bool    hit = false, pend = false;
         Rng     snap = c.rng;
+#if SP_MERGE_QUERIES
+        bool tail = false, post1 = false;
+        rgb  L_vis = mkc(0, 0, 0); // tail: L if the last light's MIS ray is unoccluded (L itself: if occluded)
+#endif
         if (alive) {
             rng_prepare(c.rng);
+#if SP_MERGE_QUERIES
+            if (!traced)
+#endif
             qr = trace(c, ray, tmin, tmax);
             if (qr.geom) {
                 wo = neg(ray.d);
@@ -2419,10 +2667,20 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
             }
 #endif
             if (hit) {
-                const rgb e    = go ? mis_material_part(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material) : mkc(0, 0, 0);
+                rgb e = mkc(0, 0, 0);
+#if SP_MERGE_QUERIES
+                rgb e_vis = mkc(0, 0, 0);
+                if (go && mq && li == c.sc.n_lights - 1) // the last light's MIS ray joins the merged pass
+                    tail = mis_material_part_mq(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material, m, e, e_vis);
+                else
+#endif
+                if (go) e = mis_material_part(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material);
                 c.rng.srv_on   = 0;
                 c.rng.srv_B    = false;
-                L              = cadd(L, cmul(throughput, e));
+#if SP_MERGE_QUERIES
+                if (tail) L_vis = cadd(L, cmul(throughput, e_vis));
+#endif
+                L = cadd(L, cmul(throughput, e));
             }
         }
         if (hit) {
@@ -2442,7 +2700,52 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
             ray.d = wi;
             tmin  = ray_offset(cosine);
             tmax  = k_infinite;
+#if SP_MERGE_QUERIES
+            if (mq && alive && depth + 1 < c.sc.max_depth) {
+                // the next bounce's trace(): intersect_lights and the unbounded shapes now, the BVH
+                // walk in the merged pass (next_o is qr.is.p: ray_at of the same ray and t)
+                ++c.rays;
+                qr.lh          = scene_intersect_lights(c.sc, ray, tmin, tmax, c.st);
+                const float tm = qr.lh.hit ? qr.lh.t : tmax;
+                const Hit   h0 = scene_intersect_unbounded(c.sc, ray, tmin, tm);
+                const int   ln = threadIdx.x & 63;
+                mq_put3(m, MQ_O, ln, ray.o);
+                mq_put3(m, MQ_D1, ln, ray.d);
+                m[MQ_T1 + ln]  = __float_as_uint(tmin);
+                m[MQ_H1T + ln] = __float_as_uint(h0.t);
+                m[MQ_H1C + ln] = h0.code;
+                post1          = true;
+            }
+#endif
         }
+#if SP_MERGE_QUERIES
+        traced = false;
+        if (mq) {
+            const uint64_t m1 = __ballot(post1), m3 = __ballot(tail);
+            if ((m1 | m3) != 0ull) {
+                const int      ln = threadIdx.x & 63;
+                const uint64_t lt = (1ull << ln) - 1ull;
+                const int      n1 = __popcll(m1);
+                uint8_t*       qs = reinterpret_cast<uint8_t*>(m + MQ_Q);
+                if (post1) qs[__popcll(m1 & lt)] = (uint8_t)ln;
+                if (tail) qs[n1 + __popcll(m3 & lt)] = (uint8_t)(ln | 0x80);
+                mq_sync();
+                SP_WPROF(5, mq_run(c.sc, c.st, m, n1 + __popcll(m3)));
+                if (tail && !mis_ray_occluded(c, m)) L = L_vis;
+                if (post1) {
+                    Hit h;
+                    h.t     = mq_f(m, MQ_D1 + ln);
+                    h.code  = m[MQ_D1 + 64 + ln];
+                    h.beta  = mq_f(m, MQ_D1 + 128 + ln);
+                    h.gamma = mq_f(m, MQ_T1 + ln);
+                    qr.geom = (h.code != 0xffffffffu);
+                    if (qr.geom) qr.is = finish_hit(c.sc, h, ray, c.q);
+                    traced = true;
+                }
+                mq_sync(); // the slots are the next serve_rho round's
+            }
+        }
+#endif
     }
     return L;
 }

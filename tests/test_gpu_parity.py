@@ -301,3 +301,22 @@ def test_rrnee_clipped_border_tiles_bitexact(scene_dir, scene, w, h, spp):
     assert gst.rays == cst["rays"] and gst.shadow_rays == cst["shadow_rays"]
     assert np.isfinite(g).all()
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [("elf_small.sp", 40, 56, 3), ("elf_small.sp", 70, 35, 2),
+                                           ("material_spheres.sp", 24, 48, 3), ("material_spheres_ibl.sp", 24, 48, 3),
+                                           ("bunny.sp", 64, 40, 2), ("lucy_small.sp", 40, 56, 2),
+                                           ("closed_room.sp", 16, 16, 2)])
+def test_rrnee_merged_queries_equal_per_lane(scene_dir, scene, w, h, spp):
+    # IterativeRRNEE on SAH scenes deals each bounce's MIS-ray and next closest-hit BVH walks over
+    # the wave (sp_path.hpp mq_run); SP_RENDER_PER_LANE_QUERIES walks every ray on its own lane.
+    # Same queries, same walks: bit-identical images and identical ray / shadow / draw counts
+    # (material_spheres: two lights -- only the last light's MIS ray joins the pass; closed_room:
+    # max_depth 40; a clipped size)
+    s = load(scene_dir, scene, w, h, bvh=0)
+    a, ast = sp.render_tiles(s, "iterative_rrnee", spp)
+    b, bst = sp.render_tiles(s, "iterative_rrnee", spp, per_lane_queries=True)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
+    assert (ast.rays, ast.shadow_rays, ast.samples, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.samples, bst.rng_draws)
+    c, _ = _oracle.render(s, sp.string_to_integrator_type("iterative_rrnee"), spp, variant="spm")
+    assert rel_l2(a, c) < REL_L2_TOL
