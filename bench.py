@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront", "chunks"])
     ap.add_argument("--waves", type=int, default=0,
                     help="megakernel occupancy variant (sp_render_params.waves_per_simd; 0 = automatic)")
+    ap.add_argument("--per-lane-queries", action="store_true",
+                    help="IterativeRRNEE: walk every ray on its own lane (SP_RENDER_PER_LANE_QUERIES; comparison)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
     ap.add_argument("--traffic-json", default=None,
@@ -245,7 +247,8 @@ def main():
             out[: len(my_tiles)] = torch.from_numpy(tiles)
             return _CpuStats(st, (time.perf_counter() - t) * 1e3)
         return sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
-                                      pipeline=args.pipeline, stage_timing=True, waves_per_simd=args.waves)
+                                      pipeline=args.pipeline, stage_timing=True, waves_per_simd=args.waves,
+                                      per_lane_queries=args.per_lane_queries)
 
     def step():
         st = render()

@@ -460,6 +460,7 @@ struct Hit {
     float    t;
     uint32_t code; // kind << 30 | index ; 0xffffffff = none
     float    beta, gamma;
+    uint32_t slot = 0xffffffffu; // 8-wide walks: wide slot of the hit primitive (none / unbounded: ~0)
 };
 
 constexpr uint32_t KIND_TRI = 0u, KIND_SPHERE = 1u, KIND_PLANE = 2u;
@@ -524,6 +525,31 @@ __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, con
     const bool   hit = (kind == KIND_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
     if (hit) { h.t = t; h.code = code; }
     return hit;
+}
+
+// Closest hit on the 8-wide BVH: (t, wide slot) is minimised lexicographically over every primitive
+// the ray hits in [tmin, t_max], so the result does not depend on the order a walk meets them --
+// the walks that several lanes share (mq_run) and the per-lane walk give the same hit.  (On the SAH
+// BVH only equal-t ties are affected, which the reference-order BVH keeps in the reference's
+// order: the binary walks use prim_closest.)  A BVH primitive at the unbounded shapes' t wins, as
+// with prim_closest (their slot is ~0).
+__device__ __forceinline__ bool prim_closest_w(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h)
+{
+    const float4   q0   = sc.wslot_tri[3 * slot]; // p0 | code
+    const uint32_t code = __float_as_uint(q0.w);
+    const uint32_t kind = code >> CODE_SHIFT;
+    float          t, be = 0.0f, ga = 0.0f;
+    bool           hit;
+    if (kind == KIND_TRI) {
+        const float4 q1 = sc.wslot_tri[3 * slot + 1], q2 = sc.wslot_tri[3 * slot + 2];
+        hit = tri_hit(q0, q1, q2, ray, tmin, h.t, t, be, ga);
+    } else {
+        const Shape& s = sc.shapes[code & CODE_MASK];
+        hit = (kind == KIND_SPHERE) ? sphere_t(s.w2o, ray, tmin, h.t, t) : plane_t(s.w2o, ray, tmin, h.t, t);
+    }
+    if (!hit || !(t < h.t || slot < h.slot)) return false;
+    h.t = t; h.code = code; h.beta = be; h.gamma = ga; h.slot = slot;
+    return true;
 }
 
 __device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, float tmax,
@@ -771,7 +797,8 @@ __device__ __forceinline__ uint32_t key_mask(uint32_t m, uint32_t o)
 // entry {child_base << 8 | key mask} with the group's smallest entry distance in the stack's
 // upper half (s[(e + depth / 2) * 64 + lane]; the upload sizes the stack for it); a group whose distance exceeds the closest hit found since is
 // dropped whole.  Every primitive whose (outward-rounded) box meets [tmin, t_closest] is tested,
-// so the result is the binary walk's except which of two primitives at exactly equal t wins.
+// so the result is the binary walk's except which of two primitives at exactly equal t wins
+// (here: the lower wide slot, prim_closest_w).
 __device__ __forceinline__ Hit wide_closest(const Scene& sc, const Ray& ray, float tmin, Hit h, Stack st)
 {
     const f3       inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
@@ -788,7 +815,7 @@ __device__ __forceinline__ Hit wide_closest(const Scene& sc, const Ray& ray, flo
             const int      k    = __ffs(m) - 1;
             const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
             const uint32_t base = wh.leaf_base + (meta & 31u);
-            for (uint32_t j = 0; j < (meta >> 5); ++j) prim_closest(sc, base + j, ray, tmin, h, sc.wslot_tri);
+            for (uint32_t j = 0; j < (meta >> 5); ++j) prim_closest_w(sc, base + j, ray, tmin, h);
         }
 #ifdef SP_WAVE_PROF
         wprof_end(6, t_it);
@@ -1669,17 +1696,17 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
 #define SP_MERGE_QUERIES 1
 #endif
 enum : int {
-    MQ_O = 0,      // shared origin of an owner's two rays (x, y, z planes of 64)
-    MQ_D3 = 192,   // MIS ray direction (estimate_direct_mis, Integrator.cpp:527-533)
-    MQ_T3 = 384,   // its t_min
-    MQ_D1 = 448,   // next bounce's direction (Integrator.cpp:570); result {t, code, beta} overwrites it
-    MQ_T1 = 640,   // its t_min; result gamma overwrites it
-    MQ_H1T = 704,  // its t_max after the light and unbounded-shape tests (the walk's starting hit)
-    MQ_H1C = 768,  // the starting hit's primitive code
-    MQ_R3 = 832,   // MIS ray's geometry any-hit result
-    MQ_Q = 896,    // queue: 128 bytes, query r = owner lane | any-hit << 7
-    MQ_CNT = 928,  // next unclaimed query
-    MQ_WORDS = 929,
+    MQ_O = 0,       // shared origin of an owner's two rays (x, y, z planes of 64)
+    MQ_D3 = 192,    // MIS ray direction (estimate_direct_mis, Integrator.cpp:527-533)
+    MQ_T3 = 384,    // its t_min
+    MQ_D1 = 448,    // next bounce's direction (Integrator.cpp:570)
+    MQ_T1 = 640,    // its t_min
+    MQ_BEST = 704,  // next bounce's closest hit so far: u64 (t bits << 32 | wide slot) per owner
+    MQ_ANY = 832,   // MIS ray's geometry any-hit result per owner
+    MQ_TB = 896,    // per walking lane: pending stack entries [bot, top) and its query (thieves read it)
+    MQ_Q = 960,     // queue: 128 bytes, query r = owner lane | any-hit << 7
+    MQ_CNT = 992,   // next unclaimed query
+    MQ_WORDS = 993,
     SRV_W = 0, SRV_REQ = 512, SRV_WORDS = 576,
     SRV_WAVE_WORDS = (SP_MERGE_QUERIES && MQ_WORDS > SRV_WORDS) ? MQ_WORDS : SRV_WORDS
 };
@@ -2376,16 +2403,24 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
 // Once a bounce's served estimates are taken, a live lane holds two ray queries that depend on
 // nothing else still to come: the MIS ray of its (last) light's estimate_direct_mis
 // (Integrator.cpp:527-533: intersect_lights, then intersect_p) and the next bounce's closest hit
-// (:558-563, direction fixed at :570).  In lock step each was a wave-wide walk whose length is
-// its slowest lane's, at the occupancy of the paths still alive (0.59-0.67).  Here the cheap
-// parts stay with the owner (the light tests and the unbounded shapes), and the BVH walks are
-// posted to LDS (rays, starting hits) and dealt over every lane of the wave -- ended paths
-// included: a lane walks one query, writes its result for the owner and claims the next
-// unclaimed one, so the pass takes about (total walk steps) / 64 plus one walk, not the sum of
-// two slowest walks.  Each query is the walk the owner would have run itself: any-hit queries
-// visit nodes in wide_any's order, closest-hit ones in wide_closest's (an any-hit query's
-// t_max is FLT_MAX, so wide_closest's distance culling never drops a group for it), with the
-// same box and primitive tests.  Results, ray counts and stream words are unchanged.
+// (:558-563, direction fixed at :570).  In lock step each was a wave-wide walk as long as its
+// slowest lane's, at the occupancy of the paths still alive (0.59-0.67).  Here the cheap parts
+// stay with the owner (the light tests, the unbounded shapes) and the BVH walks are posted to LDS
+// and shared by every lane of the wave, ended paths included:
+//   * each lane takes a query from the wave's queue and walks it (8-wide nodes, the octant order
+//     and group stack of wide_closest / wide_any);
+//   * a lane with nothing left to walk takes pending work from one that has: the OLDEST group entry
+//     of its stack (the bottom -- the biggest subtree still unvisited), and walks it for that
+//     query.  Pairs are dealt by lane order once per step, one thief per victim, so no two lanes
+//     ever touch one stack entry; the lanes' steps are one SIMT instruction stream, and each
+//     lane's stack bounds [bot, top) live in LDS (MQ_TB) for its thief.
+// A closest-hit query's answer is the lexicographic minimum of (t, wide slot) over every primitive
+// it hits (prim_closest_w: independent of which lane meets which primitive first); the lanes
+// sharing it meet in one u64 atomicMin (MQ_BEST), which also gives every one of them the current
+// t_max for its box tests and group culling.  An any-hit query ends for everyone once one lane
+// finds a hit (MQ_ANY); its t_max is FLT_MAX, so nothing is culled for it, as in wide_any.
+// Results are the per-lane walks' (SP_RENDER_PER_LANE_QUERIES: bit-identical images and counts);
+// only which lane walks which node changes.
 __device__ __forceinline__ float    mq_f(const uint32_t* m, int i) { return __uint_as_float(m[i]); }
 __device__ __forceinline__ f3       mq_f3(const uint32_t* m, int b, int o) { return mk(mq_f(m, b + o), mq_f(m, b + 64 + o), mq_f(m, b + 128 + o)); }
 __device__ __forceinline__ void     mq_put3(uint32_t* m, int b, int o, f3 v)
@@ -2394,105 +2429,160 @@ __device__ __forceinline__ void     mq_put3(uint32_t* m, int b, int o, f3 v)
     m[b + 64 + o]  = __float_as_uint(v.y);
     m[b + 128 + o] = __float_as_uint(v.z);
 }
+__device__ __forceinline__ unsigned long long* mq_best(uint32_t* m, int o)
+{
+    return reinterpret_cast<unsigned long long*>(m + MQ_BEST) + o;
+}
 __device__ __forceinline__ void mq_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+#ifndef SP_MQ_STEAL
+#define SP_MQ_STEAL 1
+#endif
+#ifndef SP_MQ_SHADOW // the shadow rays' walks shared too (mis_light_part_mq)
+#define SP_MQ_SHADOW 1
+#endif
 // All lanes in integrate() call it; total = queries in m[MQ_Q..] (posted and synchronised by the caller).
-__device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, int total)
+// any_tmax: any-hit queries' t_max is in word MQ_BEST + owner (a pass without closest-hit queries:
+// shadow rays); else FLT_MAX (MIS rays).
+__device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, int total, bool any_tmax = false)
 {
     const int      lane = threadIdx.x & 63;
+    const uint64_t lt   = (1ull << lane) - 1ull;
     const uint64_t act  = __ballot(1);
-    int            q    = __popcll(act & ((1ull << lane) - 1ull)); // first round: one query per lane present
+    int            q    = __popcll(act & lt); // first round: one query per lane present
     if (q == 0) m[MQ_CNT] = (uint32_t)__popcll(act);
     mq_sync();
     const int      half = st.depth >> 1;
     const uint8_t* qs   = reinterpret_cast<const uint8_t*>(m + MQ_Q);
-    Ray            ray;
-    f3             inv  = mk(0, 0, 0);
-    uint32_t       o    = 0, node = 0;
-    float          tmin = 0.0f;
-    Hit            h;
-    bool           any  = false;
-    int            own  = 0, sp = 0;
-    auto start = [&](int qi) {
-        const uint32_t e = qs[qi];
-        own  = (int)(e & 63u);
-        any  = (e & 0x80u) != 0u;
+    // the lane's walk: query (owner, any), node to visit, its stack [bot, sp)
+    Ray      ray;
+    f3       inv  = mk(0, 0, 0);
+    uint32_t o    = 0, node = 0;
+    float    tmin = 0.0f, amax = k_infinite;
+    bool     any  = false, has_node = false;
+    int      own  = -1, sp = 0, bot = 0;
+    auto load = [&](uint32_t e) { // query e = owner | any << 6
+        own   = (int)(e & 63u);
+        any   = (e & 64u) != 0u;
         ray.o = mq_f3(m, MQ_O, own);
         ray.d = mq_f3(m, any ? MQ_D3 : MQ_D1, own);
         tmin  = mq_f(m, (any ? MQ_T3 : MQ_T1) + own);
-        h.t    = any ? k_infinite : mq_f(m, MQ_H1T + own);
-        h.code = any ? 0xffffffffu : m[MQ_H1C + own];
-        h.beta = h.gamma = 0.0f;
-        inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-        o    = dir_sign_bits(ray.d);
-        sp   = 0;
-        node = 0;
+        amax  = (any && any_tmax) ? mq_f(m, MQ_BEST + own) : k_infinite;
+        inv   = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+        o     = dir_sign_bits(ray.d);
     };
-    bool have = q < total;
-    if (have) start(q);
-    while (have) {
+    auto take = [&](int qi) {
+        const uint32_t e = qs[qi];
+        load((e & 63u) | ((e >> 1) & 64u));
+        node = 0; has_node = true; sp = 0; bot = 0;
+        m[MQ_TB + lane] = ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
+    };
+    if (q < total) take(q);
+    while (true) {
+        if (own >= 0) {
 #ifdef SP_WAVE_PROF
-        const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 4: lanes walking, per step
+            const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 4: lanes walking, per step
 #endif
-        const WideHits wh    = wide_visit(sc, node, ray, inv, tmin, h.t);
-        bool           found = false;
-        for (uint32_t mm = wh.leaf; mm && !found; mm &= mm - 1) {
-            const int      k    = __ffs(mm) - 1;
-            const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
-            const uint32_t base = wh.leaf_base + (meta & 31u);
-            for (uint32_t j = 0; j < (meta >> 5); ++j) {
-                if (any) {
-                    if (prim_any(sc, base + j, ray, tmin, h.t, sc.wslot_tri)) { found = true; break; }
-                } else {
-                    prim_closest(sc, base + j, ray, tmin, h, sc.wslot_tri);
-                }
-            }
-        }
-        bool end = found;
-        if (!found) {
-            if (wh.inner) {
-                const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o); // octant order
-                if (rest) {
-                    st.s[sp * 64 + st.lane]          = (wh.child_base << 8) | rest;
-                    st.s[(sp + half) * 64 + st.lane] = __float_as_uint(wh.t_rest);
-                    ++sp;
-                }
-                node = wh.child_base + (uint32_t)wh.nearest;
+            bot = (int)((m[MQ_TB + lane] >> 8) & 0xffu); // a thief may have raised it
+            float tmax;
+            if (any) {
+                tmax = amax;
+                if (m[MQ_ANY + own] != 0u) { has_node = false; sp = bot; } // another lane found a hit
             } else {
-                end = true;
-                while (sp > 0) {
+                tmax = __uint_as_float((uint32_t)(*mq_best(m, own) >> 32));
+            }
+            if (!has_node) { // the next pending group child, culled by the current closest t
+                while (sp > bot) {
                     const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
-                    if (__uint_as_float(st.s[(sp - 1 + half) * 64 + st.lane]) > h.t) { --sp; continue; }
+                    if (__uint_as_float(st.s[(sp - 1 + half) * 64 + st.lane]) > tmax) { --sp; continue; }
                     uint32_t  mk8 = e & 0xffu;
                     const int k   = __ffs(mk8) - 1;
                     mk8 &= mk8 - 1;
                     if (mk8) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | mk8;
                     else --sp;
-                    node = (e >> 8) + ((uint32_t)k ^ o);
-                    end  = false;
+                    node     = (e >> 8) + ((uint32_t)k ^ o);
+                    has_node = true;
                     break;
                 }
             }
-        }
-        if (end) {
-            if (any) {
-                m[MQ_R3 + own] = found ? 1u : 0u;
-            } else { // {t, code, beta} over the direction, gamma over t_min: read by this lane only
-                m[MQ_D1 + own]       = __float_as_uint(h.t);
-                m[MQ_D1 + 64 + own]  = h.code;
-                m[MQ_D1 + 128 + own] = __float_as_uint(h.beta);
-                m[MQ_T1 + own]       = __float_as_uint(h.gamma);
+            if (has_node) {
+                const WideHits wh    = wide_visit(sc, node, ray, inv, tmin, tmax);
+                bool           found = false;
+                Hit            h;
+                h.t = tmax; h.code = 0xffffffffu; h.beta = h.gamma = 0.0f; h.slot = 0xffffffffu;
+                for (uint32_t mm = wh.leaf; mm && !found; mm &= mm - 1) {
+                    const int      k    = __ffs(mm) - 1;
+                    const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
+                    const uint32_t base = wh.leaf_base + (meta & 31u);
+                    for (uint32_t j = 0; j < (meta >> 5); ++j) {
+                        if (any) {
+                            if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) { found = true; break; }
+                        } else if (prim_closest_w(sc, base + j, ray, tmin, h)) {
+                            // first the lane's own minimum, then one atomicMin for the node
+                        }
+                    }
+                }
+                if (!any && h.slot != 0xffffffffu)
+                    atomicMin(mq_best(m, own), ((unsigned long long)__float_as_uint(h.t) << 32) | h.slot);
+                if (found) {
+                    m[MQ_ANY + own] = 1u;
+                    has_node = false;
+                    sp       = bot;
+                } else if (wh.inner) {
+                    const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o); // octant order
+                    if (rest) {
+                        st.s[sp * 64 + st.lane]          = (wh.child_base << 8) | rest;
+                        st.s[(sp + half) * 64 + st.lane] = __float_as_uint(wh.t_rest);
+                        ++sp;
+                    }
+                    node = wh.child_base + (uint32_t)wh.nearest;
+                } else {
+                    has_node = false;
+                }
             }
-            q    = (int)atomicAdd(&m[MQ_CNT], 1u);
-            have = q < total;
-            if (have) start(q);
-        }
+            if (!has_node && sp == bot) own = -1; // this lane's part of the query is done
+            m[MQ_TB + lane] = (uint32_t)sp | ((uint32_t)bot << 8) | ((uint32_t)(own & 63) << 16) | (any ? 1u << 22 : 0u);
 #ifdef SP_WAVE_PROF
-        wprof_end(4, t_it);
+            wprof_end(4, t_it);
+#endif
+        }
+        if (own < 0 && (int)m[MQ_CNT] < total) { // the queue first
+            const int qi = (int)atomicAdd(&m[MQ_CNT], 1u);
+            if (qi < total) take(qi);
+        }
+        const uint64_t idle = __ballot(own < 0);
+        if (idle == act) break; // nothing walked, nothing pending, queue empty
+#if SP_MQ_STEAL
+        uint64_t can = __ballot(own >= 0 && sp > bot); // lanes with a pending group entry
+        if (idle != 0ull && can != 0ull) {
+            mq_sync(); // the victims' stacks and bounds are in LDS
+            // pair idle lanes with victims in lane order (one thief per victim)
+            uint64_t ii = idle;
+            int      vict = -1;
+            for (int k = 0; k < 8 && ii != 0ull && can != 0ull; ++k) {
+                const int v = __ffsll((unsigned long long)can) - 1, t = __ffsll((unsigned long long)ii) - 1;
+                can &= can - 1ull;
+                ii &= ii - 1ull;
+                if (lane == t) vict = v;
+            }
+            if (vict >= 0) {
+                const uint32_t tb = m[MQ_TB + vict];
+                const int      vb = (int)((tb >> 8) & 0xffu);
+                const uint32_t e  = st.s[vb * 64 + vict];
+                const uint32_t dd = st.s[(vb + half) * 64 + vict];
+                m[MQ_TB + vict]   = (tb & ~0xff00u) | ((uint32_t)(vb + 1) << 8);
+                load(((tb >> 16) & 63u) | ((tb >> 16) & 64u));
+                st.s[st.lane]          = e; // the stolen group is this lane's whole stack
+                st.s[half * 64 + st.lane] = dd;
+                sp = 1; bot = 0; has_node = false;
+                m[MQ_TB + lane] = 1u | ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
+            }
+            mq_sync();
+        }
 #endif
     }
     mq_sync();
@@ -2542,14 +2632,51 @@ __device__ __forceinline__ bool mis_material_part_mq(Ctx& c, const Light& l, con
     }
     mq_put3(m, MQ_O, lane, p);
     mq_put3(m, MQ_D3, lane, ms.dir);
-    m[MQ_T3 + lane] = __float_as_uint(mmin);
+    m[MQ_T3 + lane]  = __float_as_uint(mmin);
+    m[MQ_ANY + lane] = 0u;
     return true;
+}
+// mis_light_part (Integrator.cpp:496-502: Light::sample, then the shadow ray's intersect_p) with the
+// shadow ray's BVH walk shared by the wave: every lane of integrate() calls it (want: this lane has
+// a hit to estimate light l at).  Same draws, counts and result as mis_light_part.
+__device__ __forceinline__ bool mis_light_part_mq(Ctx& c, const Light& l, f3 p, f3 n, LSample& ls, bool want, uint32_t* m)
+{
+    const int lane = threadIdx.x & 63;
+    bool      go = false, post = false;
+    if (want) {
+        ls = light_sample(c.sc, l, p, n, next2D(c.rng), c.q);
+        if (!(ls.pdf == 0.0f || cblack(ls.L))) {
+            ++c.shadow; // occluded(): geometry (unbounded shapes, BVH) || lights
+            ++c.rays;
+            if (!unbounded_any(c.sc, ls.ray, ls.tmin, ls.tmax)) {
+                if (c.sc.n_nodes == 0) {
+                    go = !lights_any(c.sc, ls.ray, ls.tmin, ls.tmax, c.st);
+                } else {
+                    mq_put3(m, MQ_O, lane, ls.ray.o);
+                    mq_put3(m, MQ_D3, lane, ls.ray.d);
+                    m[MQ_T3 + lane]   = __float_as_uint(ls.tmin);
+                    m[MQ_BEST + lane] = __float_as_uint(ls.tmax);
+                    m[MQ_ANY + lane]  = 0u;
+                    post              = true;
+                }
+            }
+        }
+    }
+    const uint64_t mp = __ballot(post);
+    if (mp != 0ull) {
+        if (post) reinterpret_cast<uint8_t*>(m + MQ_Q)[__popcll(mp & ((1ull << lane) - 1ull))] = (uint8_t)(lane | 0x80);
+        mq_sync();
+        SP_WPROF(5, mq_run(c.sc, c.st, m, __popcll(mp), true));
+        if (post) go = !(m[MQ_ANY + lane] != 0u || lights_any(c.sc, ls.ray, ls.tmin, ls.tmax, c.st));
+        mq_sync(); // the slots are serve_rho's next
+    }
+    return go;
 }
 // after mq_run: the MIS ray's Scene::intersect_p = the BVH walk's result || the lights
 __device__ __forceinline__ bool mis_ray_occluded(Ctx& c, const uint32_t* m)
 {
     const int lane = threadIdx.x & 63;
-    if (m[MQ_R3 + lane] != 0u) return true;
+    if (m[MQ_ANY + lane] != 0u) return true;
     Ray mr;
     mr.o = mq_f3(m, MQ_O, lane);
     mr.d = mq_f3(m, MQ_D3, lane);
@@ -2638,6 +2765,12 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
             LSample        ls;
             bool           go = false, want = false;
             const uint32_t rays0 = c.rays, shadow0 = c.shadow;
+#if SP_MERGE_QUERIES && SP_MQ_SHADOW
+            if (mq) {
+                go   = mis_light_part_mq(c, c.sc.lights[li], qr.is.p, n, ls, hit, m);
+                want = go && material_has_rho(c.sc, qr.is.material);
+            } else
+#endif
             if (hit) {
                 go   = mis_light_part(c, c.sc.lights[li], qr.is.p, n, ls);
                 want = go && material_has_rho(c.sc, qr.is.material);
@@ -2711,10 +2844,9 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
                 const int   ln = threadIdx.x & 63;
                 mq_put3(m, MQ_O, ln, ray.o);
                 mq_put3(m, MQ_D1, ln, ray.d);
-                m[MQ_T1 + ln]  = __float_as_uint(tmin);
-                m[MQ_H1T + ln] = __float_as_uint(h0.t);
-                m[MQ_H1C + ln] = h0.code;
-                post1          = true;
+                m[MQ_T1 + ln]      = __float_as_uint(tmin);
+                *mq_best(m, ln)    = ((unsigned long long)__float_as_uint(h0.t) << 32) | 0xffffffffull;
+                post1              = true;
             }
 #endif
         }
@@ -2733,11 +2865,17 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
                 SP_WPROF(5, mq_run(c.sc, c.st, m, n1 + __popcll(m3)));
                 if (tail && !mis_ray_occluded(c, m)) L = L_vis;
                 if (post1) {
+                    // the walk's answer: (t, wide slot) of the closest BVH primitive, or the
+                    // unbounded shapes' hit; the primitive's test is repeated for its code, beta, gamma
+                    const unsigned long long key = *mq_best(m, ln);
+                    const uint32_t slot = (uint32_t)key;
                     Hit h;
-                    h.t     = mq_f(m, MQ_D1 + ln);
-                    h.code  = m[MQ_D1 + 64 + ln];
-                    h.beta  = mq_f(m, MQ_D1 + 128 + ln);
-                    h.gamma = mq_f(m, MQ_T1 + ln);
+                    if (slot == 0xffffffffu) {
+                        h = scene_intersect_unbounded(c.sc, ray, tmin, qr.lh.hit ? qr.lh.t : tmax);
+                    } else {
+                        h.t = k_infinite; h.code = 0xffffffffu; h.slot = 0xffffffffu;
+                        prim_closest_w(c.sc, slot, ray, tmin, h);
+                    }
                     qr.geom = (h.code != 0xffffffffu);
                     if (qr.geom) qr.is = finish_hit(c.sc, h, ray, c.q);
                     traced = true;
