@@ -316,7 +316,7 @@ def main():
     mrays = rays / elapsed / 1e6
     msamples = samples / elapsed / 1e6
     roofline = None if cpu_render else roofline_of(stats, min(len(my_tiles) * 64, args.width * args.height), args,
-                                                   kernel_ms)
+                                                   kernel_ms, scene.device_bytes())
 
     cpu = None
     parity = None
@@ -424,12 +424,15 @@ def valu_of(args, kernel):
             "source": os.path.relpath(args.valu_json, ROOT)}
 
 
-def roofline_of(stats, pixels, args, kernel_ms):
+def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
     """Roofline of the dominant kernel: algorithmic bytes per launch / average launch duration
-    (HIP events on the render stream, recorded around every launch inside the timed region)."""
+    (HIP events on the render stream, recorded around every launch inside the timed region).
+    Algorithmic bytes: the RNG state traffic (24 B per draw), the output, and the resident scene
+    (BVH nodes, primitive records, normals, ...) read at least once per frame -- 22 MB for bunny,
+    ~2 GB for lucy's 28 M triangles, which do not fit the 256 MiB Infinity Cache."""
     st = stats[-1]
     n = len(stats)
-    traffic = None
+    traffic, tj = None, None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as fh:
@@ -437,16 +440,21 @@ def roofline_of(stats, pixels, args, kernel_ms):
             if (tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp
                     and tj.get("scene", "bunny") == args.scene and tj.get("sim_world", 0) == args.sim_world):
                 traffic = tj.get("hbm_bytes_per_launch")
+            else:
+                tj = None
         except Exception:
-            traffic = None
+            traffic, tj = None, None
     if st.pipeline == 3:  # sample chunks (sp_chunk.hip): four kernels per frame, timed together
         samples = st.samples
         # draws at 24 B (read + the twist of its generation), the hit record written once and read
         # by ck_count and ck_shade, the 2-byte draw count, radiance written once and summed
-        alg = st.rng_draws * MT_BYTES_PER_DRAW + samples * (16 * 3 + 2 * 2 + 12 * 2) + pixels * PIXEL_BYTES
+        alg = st.rng_draws * MT_BYTES_PER_DRAW + samples * (16 * 3 + 2 * 2 + 12 * 2) + pixels * PIXEL_BYTES + scene_bytes
         achieved = alg / (kernel_ms * 1e-3) / 1e9
+        if tj is not None:  # the four kernels of the frame together, like the time
+            traffic = sum(v["hbm_bytes_per_launch"] for k, v in tj.get("kernels", {}).items() if k.startswith("ck_")) or traffic
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "ck_camera+ck_count+ck_shade+ck_sum",
+                "scene_bytes": scene_bytes,
                 "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg,
                 "valu": valu_of(args, "ck_shade")}  # the shading kernel: most of the four kernels' time
     if st.pipeline == 1 or args.integrator != "direct_lighting":  # megakernel
@@ -456,10 +464,13 @@ def roofline_of(stats, pixels, args, kernel_ms):
         probe_ms = sum(s.stage_ms[1] for s in stats) / n
         if not render_ms > 0:
             render_ms, probe_ms = kernel_ms, 0.0
-        alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES
+        alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES + scene_bytes
         achieved = alg / (render_ms * 1e-3) / 1e9
+        if tj is not None and "sp_render_kernel" in tj.get("kernels", {}):
+            traffic = tj["kernels"]["sp_render_kernel"]["hbm_bytes_per_launch"]
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "sp_render_kernel",
+                "scene_bytes": scene_bytes,
                 "kernel_ms": round(render_ms, 3), "probe_ms": round(probe_ms, 3), "alg_bytes_per_launch": alg,
                 "valu": valu_of(args, "sp_render_kernel")}
     names = ["wf_init+wf_resolve", "wf_primary", "wf_shade", "wf_shadow"]

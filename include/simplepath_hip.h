@@ -319,6 +319,9 @@ int  sp_render_tiles_host(sp_scene* scene, const sp_render_params* params, float
                           sp_render_stats* stats);
 /* BVH statistics of the uploaded scene (depth, node count, primitive slots). */
 int  sp_scene_bvh_info(const sp_scene* scene, int32_t* depth, int64_t* nodes, int64_t* slots);
+/* ABI 5: bytes the uploaded scene occupies in HBM (BVHs, primitive records, normals, materials,
+ * lights, image-light tables, RSQRTSS table) -- what a frame streams at least once. */
+int  sp_scene_device_bytes(const sp_scene* scene, int64_t* bytes);
 /* Host only (no device needed): build the geometry BVH sp_scene_upload would build for bvh_mode
  * and report its statistics; nothing is uploaded. */
 int  sp_scene_bvh_build_info(const sp_scene* scene, int32_t bvh_mode, sp_bvh_info* out);

@@ -137,6 +137,12 @@ class Scene:
         check(lib().sp_scene_bvh_info(self._h, C.byref(d), C.byref(n), C.byref(s)))
         return {"depth": d.value, "nodes": n.value, "slots": s.value}
 
+    def device_bytes(self) -> int:
+        """HBM bytes of the uploaded scene (sp_scene_device_bytes)."""
+        b = C.c_int64()
+        check(lib().sp_scene_device_bytes(self._h, C.byref(b)))
+        return b.value
+
     def bvh_build_info(self, bvh_mode: int = 0) -> dict:
         """Host-only BVH build statistics (no device): what upload(bvh_mode) would build."""
         i = _abi.sp_bvh_info()

@@ -143,6 +143,7 @@ SIGNATURES = {
     "sp_render_tiles_host": (C.c_int, [C.c_void_p, C.POINTER(sp_render_params), C.POINTER(C.c_float),
                                        C.POINTER(sp_render_stats)]),
     "sp_scene_bvh_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "sp_scene_device_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
     "sp_scene_bvh_build_info": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(sp_bvh_info)]),
     "sp_tiles_to_image": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int64,
                                     C.POINTER(C.c_float), C.POINTER(C.c_float)]),

@@ -1503,6 +1503,15 @@ int sp_scene_bvh_build_info(const sp_scene* s, int32_t bvh_mode, sp_bvh_info* ou
     }
 }
 
+int sp_scene_device_bytes(const sp_scene* s, int64_t* bytes)
+{
+    if (!s || !bytes || s->device < 0) return fail(SP_ERR_STATE, "scene not uploaded");
+    int64_t b = 0;
+    for (const auto& d : s->bufs) b += (int64_t)d.bytes;
+    *bytes = b;
+    return SP_OK;
+}
+
 int sp_scene_bvh_info(const sp_scene* s, int32_t* depth, int64_t* nodes, int64_t* slots)
 {
     if (!s || s->device < 0) return fail(SP_ERR_STATE, "scene not uploaded");

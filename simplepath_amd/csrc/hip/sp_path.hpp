@@ -1706,11 +1706,12 @@ enum : int {
     MQ_TB = 896,    // per walking lane: pending stack entries [bot, top) and its query (thieves read it)
     MQ_Q = 960,     // queue: 128 bytes, query r = owner lane | any-hit << 7
     MQ_CNT = 992,   // next unclaimed query
-    MQ_WORDS = 993,
+    MQ_WORDS = 996, // a multiple of 4: every wave's row, and MQ_BEST's u64 slots, stay 16-byte aligned
     SRV_W = 0, SRV_REQ = 512, SRV_WORDS = 576,
     SRV_WAVE_WORDS = (SP_MERGE_QUERIES && MQ_WORDS > SRV_WORDS) ? MQ_WORDS : SRV_WORDS
 };
-static __shared__ uint32_t srv_lds[4][SRV_WAVE_WORDS];
+static_assert(SRV_WAVE_WORDS % 4 == 0 && MQ_BEST % 2 == 0, "u64 LDS atomics need 8-byte alignment");
+static __shared__ __attribute__((aligned(16))) uint32_t srv_lds[4][SRV_WAVE_WORDS];
 __device__ __forceinline__ float*   srv_w_at(int wave, int k, int j) { return reinterpret_cast<float*>(&srv_lds[wave][SRV_W + (k * 2 + j) * 64]); }
 __device__ __forceinline__ uint8_t* srv_req_of(int wave) { return reinterpret_cast<uint8_t*>(&srv_lds[wave][SRV_REQ]); }
 #endif
