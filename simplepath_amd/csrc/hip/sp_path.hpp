@@ -848,6 +848,201 @@ __device__ __forceinline__ Hit wide_closest(const Scene& sc, const Ray& ray, flo
     return h;
 }
 
+// ---------------------------------------------------------------- merged query pass
+// Once a bounce's served estimates are taken, a live lane holds two ray queries that depend on
+// nothing else still to come: the MIS ray of its (last) light's estimate_direct_mis
+// (Integrator.cpp:527-533: intersect_lights, then intersect_p) and the next bounce's closest hit
+// (:558-563, direction fixed at :570).  In lock step each was a wave-wide walk as long as its
+// slowest lane's, at the occupancy of the paths still alive (0.59-0.67).  Here the cheap parts
+// stay with the owner (the light tests, the unbounded shapes) and the BVH walks are posted to LDS
+// and shared by every lane of the wave, ended paths included:
+//   * each lane takes a query from the wave's queue and walks it (8-wide nodes, the octant order
+//     and group stack of wide_closest / wide_any);
+//   * a lane with nothing left to walk takes pending work from one that has: the OLDEST group entry
+//     of its stack (the bottom -- the biggest subtree still unvisited), and walks it for that
+//     query.  Pairs are dealt by lane order once per step, one thief per victim, so no two lanes
+//     ever touch one stack entry; the lanes' steps are one SIMT instruction stream, and each
+//     lane's stack bounds [bot, top) live in LDS (MQ_TB) for its thief.
+// A closest-hit query's answer is the lexicographic minimum of (t, wide slot) over every primitive
+// it hits (prim_closest_w: independent of which lane meets which primitive first); the lanes
+// sharing it meet in one u64 atomicMin (MQ_BEST), which also gives every one of them the current
+// t_max for its box tests and group culling.  An any-hit query ends for everyone once one lane
+// finds a hit (MQ_ANY); its t_max is FLT_MAX, so nothing is culled for it, as in wide_any.
+// Results are the per-lane walks' (SP_RENDER_PER_LANE_QUERIES: bit-identical images and counts);
+// only which lane walks which node changes.
+__device__ __forceinline__ float    mq_f(const uint32_t* m, int i) { return __uint_as_float(m[i]); }
+__device__ __forceinline__ f3       mq_f3(const uint32_t* m, int b, int o) { return mk(mq_f(m, b + o), mq_f(m, b + 64 + o), mq_f(m, b + 128 + o)); }
+__device__ __forceinline__ void     mq_put3(uint32_t* m, int b, int o, f3 v)
+{
+    m[b + o]       = __float_as_uint(v.x);
+    m[b + 64 + o]  = __float_as_uint(v.y);
+    m[b + 128 + o] = __float_as_uint(v.z);
+}
+template <class L>
+__device__ __forceinline__ unsigned long long* mq_best(uint32_t* m, int o)
+{
+    return reinterpret_cast<unsigned long long*>(m + L::BEST) + o;
+}
+__device__ __forceinline__ void mq_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#ifndef SP_MQ_STEAL
+#define SP_MQ_STEAL 1
+#endif
+// The per-wave LDS rows a shared walk uses: L::O / D3 / T3 the any-hit rays (origin, direction,
+// t_min), L::AMAX their t_max, L::ANY their results; L::D1 / T1 the closest-hit rays (origin in
+// L::O too), L::BEST their u64 (t, wide slot) answers; L::TB the walking lanes' stack bounds and
+// queries, L::Q the queue (query r = owner lane | any-hit << 7), L::CNT its next unclaimed entry.
+// All lanes in integrate() call it; total = queries in m[L::Q..] (posted and synchronised by the
+// caller).  any_tmax: any-hit queries' t_max is in m[L::AMAX + owner]; else FLT_MAX (MIS rays).
+// ANY_ONLY: no closest-hit query is ever posted (the closest-hit code is not compiled).
+template <class L, bool ANY_ONLY = false>
+__device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, int total, bool any_tmax = false)
+{
+    const int      lane = threadIdx.x & 63;
+    const uint64_t lt   = (1ull << lane) - 1ull;
+    const uint64_t act  = __ballot(1);
+    int            q    = __popcll(act & lt); // first round: one query per lane present
+    if (q == 0) m[L::CNT] = (uint32_t)__popcll(act);
+    mq_sync();
+    const int      half = st.depth >> 1;
+    const uint8_t* qs   = reinterpret_cast<const uint8_t*>(m + L::Q);
+    // the lane's walk: query (owner, any), node to visit, its stack [bot, sp)
+    Ray      ray;
+    f3       inv  = mk(0, 0, 0);
+    uint32_t o    = 0, node = 0;
+    float    tmin = 0.0f, amax = k_infinite;
+    bool     any  = false, has_node = false;
+    int      own  = -1, sp = 0, bot = 0;
+    auto load = [&](uint32_t e) { // query e = owner | any << 6
+        own   = (int)(e & 63u);
+        any   = ANY_ONLY || (e & 64u) != 0u;
+        ray.o = mq_f3(m, L::O, own);
+        ray.d = mq_f3(m, any ? L::D3 : L::D1, own);
+        tmin  = mq_f(m, (any ? L::T3 : L::T1) + own);
+        amax  = (any && any_tmax) ? mq_f(m, L::AMAX + own) : k_infinite;
+        inv   = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+        o     = dir_sign_bits(ray.d);
+    };
+    auto take = [&](int qi) {
+        const uint32_t e = qs[qi];
+        load((e & 63u) | ((e >> 1) & 64u));
+        node = 0; has_node = true; sp = 0; bot = 0;
+        m[L::TB + lane] = ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
+    };
+    if (q < total) take(q);
+    while (true) {
+        if (own >= 0) {
+#ifdef SP_WAVE_PROF
+            const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 4: lanes walking, per step
+#endif
+            bot = (int)((m[L::TB + lane] >> 8) & 0xffu); // a thief may have raised it
+            float tmax;
+            if (any) {
+                tmax = amax;
+                if (m[L::ANY + own] != 0u) { has_node = false; sp = bot; } // another lane found a hit
+            } else {
+                if constexpr (!ANY_ONLY) tmax = __uint_as_float((uint32_t)(*mq_best<L>(m, own) >> 32));
+                else tmax = amax;
+            }
+            if (!has_node) { // the next pending group child, culled by the current closest t
+                while (sp > bot) {
+                    const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
+                    if (__uint_as_float(st.s[(sp - 1 + half) * 64 + st.lane]) > tmax) { --sp; continue; }
+                    uint32_t  mk8 = e & 0xffu;
+                    const int k   = __ffs(mk8) - 1;
+                    mk8 &= mk8 - 1;
+                    if (mk8) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | mk8;
+                    else --sp;
+                    node     = (e >> 8) + ((uint32_t)k ^ o);
+                    has_node = true;
+                    break;
+                }
+            }
+            if (has_node) {
+                const WideHits wh    = wide_visit(sc, node, ray, inv, tmin, tmax);
+                bool           found = false;
+                Hit            h;
+                h.t = tmax; h.code = 0xffffffffu; h.beta = h.gamma = 0.0f; h.slot = 0xffffffffu;
+                for (uint32_t mm = wh.leaf; mm && !found; mm &= mm - 1) {
+                    const int      k    = __ffs(mm) - 1;
+                    const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
+                    const uint32_t base = wh.leaf_base + (meta & 31u);
+                    for (uint32_t j = 0; j < (meta >> 5); ++j) {
+                        if (any) {
+                            if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) { found = true; break; }
+                        } else if constexpr (!ANY_ONLY) {
+                            prim_closest_w(sc, base + j, ray, tmin, h); // the lane's minimum over the node
+                        }
+                    }
+                }
+                if constexpr (!ANY_ONLY) {
+                    if (!any && h.slot != 0xffffffffu)
+                        atomicMin(mq_best<L>(m, own), ((unsigned long long)__float_as_uint(h.t) << 32) | h.slot);
+                }
+                if (found) {
+                    m[L::ANY + own] = 1u;
+                    has_node = false;
+                    sp       = bot;
+                } else if (wh.inner) {
+                    const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o); // octant order
+                    if (rest) {
+                        st.s[sp * 64 + st.lane]          = (wh.child_base << 8) | rest;
+                        st.s[(sp + half) * 64 + st.lane] = __float_as_uint(wh.t_rest);
+                        ++sp;
+                    }
+                    node = wh.child_base + (uint32_t)wh.nearest;
+                } else {
+                    has_node = false;
+                }
+            }
+            if (!has_node && sp == bot) own = -1; // this lane's part of the query is done
+            m[L::TB + lane] = (uint32_t)sp | ((uint32_t)bot << 8) | ((uint32_t)(own & 63) << 16) | (any ? 1u << 22 : 0u);
+#ifdef SP_WAVE_PROF
+            wprof_end(4, t_it);
+#endif
+        }
+        if (own < 0 && (int)m[L::CNT] < total) { // the queue first
+            const int qi = (int)atomicAdd(&m[L::CNT], 1u);
+            if (qi < total) take(qi);
+        }
+        const uint64_t idle = __ballot(own < 0);
+        if (idle == act) break; // nothing walked, nothing pending, queue empty
+#if SP_MQ_STEAL
+        uint64_t can = __ballot(own >= 0 && sp > bot); // lanes with a pending group entry
+        if (idle != 0ull && can != 0ull) {
+            mq_sync(); // the victims' stacks and bounds are in LDS
+            // pair idle lanes with victims in lane order (one thief per victim)
+            uint64_t ii = idle;
+            int      vict = -1;
+            for (int k = 0; k < 8 && ii != 0ull && can != 0ull; ++k) {
+                const int v = __ffsll((unsigned long long)can) - 1, t = __ffsll((unsigned long long)ii) - 1;
+                can &= can - 1ull;
+                ii &= ii - 1ull;
+                if (lane == t) vict = v;
+            }
+            if (vict >= 0) {
+                const uint32_t tb = m[L::TB + vict];
+                const int      vb = (int)((tb >> 8) & 0xffu);
+                const uint32_t e  = st.s[vb * 64 + vict];
+                const uint32_t dd = st.s[(vb + half) * 64 + vict];
+                m[L::TB + vict]   = (tb & ~0xff00u) | ((uint32_t)(vb + 1) << 8);
+                load(((tb >> 16) & 63u) | ((tb >> 16) & 64u));
+                st.s[st.lane]          = e; // the stolen group is this lane's whole stack
+                st.s[half * 64 + st.lane] = dd;
+                sp = 1; bot = 0; has_node = false;
+                m[L::TB + lane] = 1u | ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
+            }
+            mq_sync();
+        }
+#endif
+    }
+    mq_sync();
+}
+
 // Wave-uniform record fetch through the constant address space: with the address in SGPRs
 // the compiler emits s_load (scalar cache).  A uniform-address VECTOR load still costs the
 // vector L1 a per-lane access (TCP_TOTAL_ACCESSES), which is what bounds the traversal kernels.
@@ -1711,6 +1906,13 @@ enum : int {
     SRV_WAVE_WORDS = (SP_MERGE_QUERIES && MQ_WORDS > SRV_WORDS) ? MQ_WORDS : SRV_WORDS
 };
 static_assert(SRV_WAVE_WORDS % 4 == 0 && MQ_BEST % 2 == 0, "u64 LDS atomics need 8-byte alignment");
+struct MqLayout { // IterativeRRNEE's rows for mq_run (the MIS / next-closest pass and the shadow pass)
+    enum : int { O = MQ_O, D3 = MQ_D3, T3 = MQ_T3, D1 = MQ_D1, T1 = MQ_T1, BEST = MQ_BEST, AMAX = MQ_BEST, ANY = MQ_ANY,
+                 TB = MQ_TB, Q = MQ_Q, CNT = MQ_CNT };
+};
+#ifndef SP_MQ_SHADOW // the shadow rays' walks shared too (mis_light_part_mq)
+#define SP_MQ_SHADOW 1
+#endif
 static __shared__ __attribute__((aligned(16))) uint32_t srv_lds[4][SRV_WAVE_WORDS];
 __device__ __forceinline__ float*   srv_w_at(int wave, int k, int j) { return reinterpret_cast<float*>(&srv_lds[wave][SRV_W + (k * 2 + j) * 64]); }
 __device__ __forceinline__ uint8_t* srv_req_of(int wave) { return reinterpret_cast<uint8_t*>(&srv_lds[wave][SRV_REQ]); }
@@ -2400,195 +2602,6 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
 }
 
 #if SP_MERGE_QUERIES
-// ---------------------------------------------------------------- merged query pass
-// Once a bounce's served estimates are taken, a live lane holds two ray queries that depend on
-// nothing else still to come: the MIS ray of its (last) light's estimate_direct_mis
-// (Integrator.cpp:527-533: intersect_lights, then intersect_p) and the next bounce's closest hit
-// (:558-563, direction fixed at :570).  In lock step each was a wave-wide walk as long as its
-// slowest lane's, at the occupancy of the paths still alive (0.59-0.67).  Here the cheap parts
-// stay with the owner (the light tests, the unbounded shapes) and the BVH walks are posted to LDS
-// and shared by every lane of the wave, ended paths included:
-//   * each lane takes a query from the wave's queue and walks it (8-wide nodes, the octant order
-//     and group stack of wide_closest / wide_any);
-//   * a lane with nothing left to walk takes pending work from one that has: the OLDEST group entry
-//     of its stack (the bottom -- the biggest subtree still unvisited), and walks it for that
-//     query.  Pairs are dealt by lane order once per step, one thief per victim, so no two lanes
-//     ever touch one stack entry; the lanes' steps are one SIMT instruction stream, and each
-//     lane's stack bounds [bot, top) live in LDS (MQ_TB) for its thief.
-// A closest-hit query's answer is the lexicographic minimum of (t, wide slot) over every primitive
-// it hits (prim_closest_w: independent of which lane meets which primitive first); the lanes
-// sharing it meet in one u64 atomicMin (MQ_BEST), which also gives every one of them the current
-// t_max for its box tests and group culling.  An any-hit query ends for everyone once one lane
-// finds a hit (MQ_ANY); its t_max is FLT_MAX, so nothing is culled for it, as in wide_any.
-// Results are the per-lane walks' (SP_RENDER_PER_LANE_QUERIES: bit-identical images and counts);
-// only which lane walks which node changes.
-__device__ __forceinline__ float    mq_f(const uint32_t* m, int i) { return __uint_as_float(m[i]); }
-__device__ __forceinline__ f3       mq_f3(const uint32_t* m, int b, int o) { return mk(mq_f(m, b + o), mq_f(m, b + 64 + o), mq_f(m, b + 128 + o)); }
-__device__ __forceinline__ void     mq_put3(uint32_t* m, int b, int o, f3 v)
-{
-    m[b + o]       = __float_as_uint(v.x);
-    m[b + 64 + o]  = __float_as_uint(v.y);
-    m[b + 128 + o] = __float_as_uint(v.z);
-}
-__device__ __forceinline__ unsigned long long* mq_best(uint32_t* m, int o)
-{
-    return reinterpret_cast<unsigned long long*>(m + MQ_BEST) + o;
-}
-__device__ __forceinline__ void mq_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-#ifndef SP_MQ_STEAL
-#define SP_MQ_STEAL 1
-#endif
-#ifndef SP_MQ_SHADOW // the shadow rays' walks shared too (mis_light_part_mq)
-#define SP_MQ_SHADOW 1
-#endif
-// All lanes in integrate() call it; total = queries in m[MQ_Q..] (posted and synchronised by the caller).
-// any_tmax: any-hit queries' t_max is in word MQ_BEST + owner (a pass without closest-hit queries:
-// shadow rays); else FLT_MAX (MIS rays).
-__device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, int total, bool any_tmax = false)
-{
-    const int      lane = threadIdx.x & 63;
-    const uint64_t lt   = (1ull << lane) - 1ull;
-    const uint64_t act  = __ballot(1);
-    int            q    = __popcll(act & lt); // first round: one query per lane present
-    if (q == 0) m[MQ_CNT] = (uint32_t)__popcll(act);
-    mq_sync();
-    const int      half = st.depth >> 1;
-    const uint8_t* qs   = reinterpret_cast<const uint8_t*>(m + MQ_Q);
-    // the lane's walk: query (owner, any), node to visit, its stack [bot, sp)
-    Ray      ray;
-    f3       inv  = mk(0, 0, 0);
-    uint32_t o    = 0, node = 0;
-    float    tmin = 0.0f, amax = k_infinite;
-    bool     any  = false, has_node = false;
-    int      own  = -1, sp = 0, bot = 0;
-    auto load = [&](uint32_t e) { // query e = owner | any << 6
-        own   = (int)(e & 63u);
-        any   = (e & 64u) != 0u;
-        ray.o = mq_f3(m, MQ_O, own);
-        ray.d = mq_f3(m, any ? MQ_D3 : MQ_D1, own);
-        tmin  = mq_f(m, (any ? MQ_T3 : MQ_T1) + own);
-        amax  = (any && any_tmax) ? mq_f(m, MQ_BEST + own) : k_infinite;
-        inv   = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-        o     = dir_sign_bits(ray.d);
-    };
-    auto take = [&](int qi) {
-        const uint32_t e = qs[qi];
-        load((e & 63u) | ((e >> 1) & 64u));
-        node = 0; has_node = true; sp = 0; bot = 0;
-        m[MQ_TB + lane] = ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
-    };
-    if (q < total) take(q);
-    while (true) {
-        if (own >= 0) {
-#ifdef SP_WAVE_PROF
-            const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 4: lanes walking, per step
-#endif
-            bot = (int)((m[MQ_TB + lane] >> 8) & 0xffu); // a thief may have raised it
-            float tmax;
-            if (any) {
-                tmax = amax;
-                if (m[MQ_ANY + own] != 0u) { has_node = false; sp = bot; } // another lane found a hit
-            } else {
-                tmax = __uint_as_float((uint32_t)(*mq_best(m, own) >> 32));
-            }
-            if (!has_node) { // the next pending group child, culled by the current closest t
-                while (sp > bot) {
-                    const uint32_t e = st.s[(sp - 1) * 64 + st.lane];
-                    if (__uint_as_float(st.s[(sp - 1 + half) * 64 + st.lane]) > tmax) { --sp; continue; }
-                    uint32_t  mk8 = e & 0xffu;
-                    const int k   = __ffs(mk8) - 1;
-                    mk8 &= mk8 - 1;
-                    if (mk8) st.s[(sp - 1) * 64 + st.lane] = (e & ~0xffu) | mk8;
-                    else --sp;
-                    node     = (e >> 8) + ((uint32_t)k ^ o);
-                    has_node = true;
-                    break;
-                }
-            }
-            if (has_node) {
-                const WideHits wh    = wide_visit(sc, node, ray, inv, tmin, tmax);
-                bool           found = false;
-                Hit            h;
-                h.t = tmax; h.code = 0xffffffffu; h.beta = h.gamma = 0.0f; h.slot = 0xffffffffu;
-                for (uint32_t mm = wh.leaf; mm && !found; mm &= mm - 1) {
-                    const int      k    = __ffs(mm) - 1;
-                    const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
-                    const uint32_t base = wh.leaf_base + (meta & 31u);
-                    for (uint32_t j = 0; j < (meta >> 5); ++j) {
-                        if (any) {
-                            if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) { found = true; break; }
-                        } else if (prim_closest_w(sc, base + j, ray, tmin, h)) {
-                            // first the lane's own minimum, then one atomicMin for the node
-                        }
-                    }
-                }
-                if (!any && h.slot != 0xffffffffu)
-                    atomicMin(mq_best(m, own), ((unsigned long long)__float_as_uint(h.t) << 32) | h.slot);
-                if (found) {
-                    m[MQ_ANY + own] = 1u;
-                    has_node = false;
-                    sp       = bot;
-                } else if (wh.inner) {
-                    const uint32_t rest = key_mask(wh.inner & ~(1u << wh.nearest), o); // octant order
-                    if (rest) {
-                        st.s[sp * 64 + st.lane]          = (wh.child_base << 8) | rest;
-                        st.s[(sp + half) * 64 + st.lane] = __float_as_uint(wh.t_rest);
-                        ++sp;
-                    }
-                    node = wh.child_base + (uint32_t)wh.nearest;
-                } else {
-                    has_node = false;
-                }
-            }
-            if (!has_node && sp == bot) own = -1; // this lane's part of the query is done
-            m[MQ_TB + lane] = (uint32_t)sp | ((uint32_t)bot << 8) | ((uint32_t)(own & 63) << 16) | (any ? 1u << 22 : 0u);
-#ifdef SP_WAVE_PROF
-            wprof_end(4, t_it);
-#endif
-        }
-        if (own < 0 && (int)m[MQ_CNT] < total) { // the queue first
-            const int qi = (int)atomicAdd(&m[MQ_CNT], 1u);
-            if (qi < total) take(qi);
-        }
-        const uint64_t idle = __ballot(own < 0);
-        if (idle == act) break; // nothing walked, nothing pending, queue empty
-#if SP_MQ_STEAL
-        uint64_t can = __ballot(own >= 0 && sp > bot); // lanes with a pending group entry
-        if (idle != 0ull && can != 0ull) {
-            mq_sync(); // the victims' stacks and bounds are in LDS
-            // pair idle lanes with victims in lane order (one thief per victim)
-            uint64_t ii = idle;
-            int      vict = -1;
-            for (int k = 0; k < 8 && ii != 0ull && can != 0ull; ++k) {
-                const int v = __ffsll((unsigned long long)can) - 1, t = __ffsll((unsigned long long)ii) - 1;
-                can &= can - 1ull;
-                ii &= ii - 1ull;
-                if (lane == t) vict = v;
-            }
-            if (vict >= 0) {
-                const uint32_t tb = m[MQ_TB + vict];
-                const int      vb = (int)((tb >> 8) & 0xffu);
-                const uint32_t e  = st.s[vb * 64 + vict];
-                const uint32_t dd = st.s[(vb + half) * 64 + vict];
-                m[MQ_TB + vict]   = (tb & ~0xff00u) | ((uint32_t)(vb + 1) << 8);
-                load(((tb >> 16) & 63u) | ((tb >> 16) & 64u));
-                st.s[st.lane]          = e; // the stolen group is this lane's whole stack
-                st.s[half * 64 + st.lane] = dd;
-                sp = 1; bot = 0; has_node = false;
-                m[MQ_TB + lane] = 1u | ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
-            }
-            mq_sync();
-        }
-#endif
-    }
-    mq_sync();
-}
-
 // mis_material_part (estimate_direct_mis after its shadow ray, Integrator.cpp:505-535) with the MIS
 // ray's occlusion test left to the merged pass: true when its BVH walk was posted (origin,
 // direction, t_min in the owner's MQ_O / MQ_D3 / MQ_T3 slots).  e_occ is the estimate if that ray
@@ -2667,7 +2680,7 @@ __device__ __forceinline__ bool mis_light_part_mq(Ctx& c, const Light& l, f3 p, 
     if (mp != 0ull) {
         if (post) reinterpret_cast<uint8_t*>(m + MQ_Q)[__popcll(mp & ((1ull << lane) - 1ull))] = (uint8_t)(lane | 0x80);
         mq_sync();
-        SP_WPROF(5, mq_run(c.sc, c.st, m, __popcll(mp), true));
+        SP_WPROF(5, mq_run<MqLayout>(c.sc, c.st, m, __popcll(mp), true));
         if (post) go = !(m[MQ_ANY + lane] != 0u || lights_any(c.sc, ls.ray, ls.tmin, ls.tmax, c.st));
         mq_sync(); // the slots are serve_rho's next
     }
@@ -2846,7 +2859,7 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
                 mq_put3(m, MQ_O, ln, ray.o);
                 mq_put3(m, MQ_D1, ln, ray.d);
                 m[MQ_T1 + ln]      = __float_as_uint(tmin);
-                *mq_best(m, ln)    = ((unsigned long long)__float_as_uint(h0.t) << 32) | 0xffffffffull;
+                *mq_best<MqLayout>(m, ln)    = ((unsigned long long)__float_as_uint(h0.t) << 32) | 0xffffffffull;
                 post1              = true;
             }
 #endif
@@ -2863,12 +2876,12 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
                 if (post1) qs[__popcll(m1 & lt)] = (uint8_t)ln;
                 if (tail) qs[n1 + __popcll(m3 & lt)] = (uint8_t)(ln | 0x80);
                 mq_sync();
-                SP_WPROF(5, mq_run(c.sc, c.st, m, n1 + __popcll(m3)));
+                SP_WPROF(5, mq_run<MqLayout>(c.sc, c.st, m, n1 + __popcll(m3)));
                 if (tail && !mis_ray_occluded(c, m)) L = L_vis;
                 if (post1) {
                     // the walk's answer: (t, wide slot) of the closest BVH primitive, or the
                     // unbounded shapes' hit; the primitive's test is repeated for its code, beta, gamma
-                    const unsigned long long key = *mq_best(m, ln);
+                    const unsigned long long key = *mq_best<MqLayout>(m, ln);
                     const uint32_t slot = (uint32_t)key;
                     Hit h;
                     if (slot == 0xffffffffu) {
