@@ -899,6 +899,9 @@ __device__ __forceinline__ void mq_sync()
 // All lanes in integrate() call it; total = queries in m[L::Q..] (posted and synchronised by the
 // caller).  any_tmax: any-hit queries' t_max is in m[L::AMAX + owner]; else FLT_MAX (MIS rays).
 // ANY_ONLY: no closest-hit query is ever posted (the closest-hit code is not compiled).
+#ifndef SP_MQ_PAIRS // thief / victim pairs dealt per walk step: elf 1024^2 @ 16 spp 879-884 at 8, 890-893 at 16 and 64
+#define SP_MQ_PAIRS 16
+#endif
 template <class L, bool ANY_ONLY = false>
 __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, int total, bool any_tmax = false)
 {
@@ -1018,7 +1021,7 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
             // pair idle lanes with victims in lane order (one thief per victim)
             uint64_t ii = idle;
             int      vict = -1;
-            for (int k = 0; k < 8 && ii != 0ull && can != 0ull; ++k) {
+            for (int k = 0; k < SP_MQ_PAIRS && ii != 0ull && can != 0ull; ++k) {
                 const int v = __ffsll((unsigned long long)can) - 1, t = __ffsll((unsigned long long)ii) - 1;
                 can &= can - 1ull;
                 ii &= ii - 1ull;
