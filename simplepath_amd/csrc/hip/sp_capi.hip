@@ -956,7 +956,7 @@ static ChunkPlan chunk_plan(const sp_scene* s, int64_t n_tiles, uint32_t spp, in
     const size_t n_px = (size_t)n_tiles * 64;
     c.b_hits  = n_px * spp * 16;
     c.b_L     = n_px * spp * 12;
-    c.b_snap  = (size_t)n_tiles * c.gens * spm::MT_N * 64 * 8;
+    c.b_snap  = (size_t)n_tiles * c.gens * spd::MT_GEN_WORDS * 8;
     c.b_ctl   = (size_t)c.chunks * n_px * 4;
     c.b_draws = c.known_draws ? n_px * spp * 2 : 0;
     c.total   = c.b_hits + c.b_L + c.b_snap + c.b_ctl + c.b_draws + 4 * 256;
@@ -1120,7 +1120,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         w.n        = (int64_t)n;
         w.tiles_x  = (s->dev.width + 7) / 8;
         w.spp      = p->samples_per_pixel;
-        w.mt_state = reinterpret_cast<uint64_t*>(take(n * 2 * spm::MT_N * 8));
+        w.mt_state = reinterpret_cast<uint64_t*>(take(n / 64 * 2 * spd::MT_GEN_WORDS * 8));
         w.sh       = reinterpret_cast<float4*>(take(n * (size_t)std::max(1, s->dev.n_lights) * 32));
         w.hit      = reinterpret_cast<float4*>(take(n * 16));
         w.shp      = reinterpret_cast<float4*>(take(n * 16));
@@ -1271,7 +1271,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         if (waves > s->mt_waves) {
             if (s->mt_state) (void)hipFree(s->mt_state);
             s->mt_state = nullptr;
-            SP_HIP(hipMalloc(&s->mt_state, waves * 2 * spm::MT_N * 64 * sizeof(uint64_t)));
+            SP_HIP(hipMalloc(&s->mt_state, waves * 2 * (size_t)spd::MT_GEN_WORDS * sizeof(uint64_t)));
             s->mt_waves = waves;
         }
         SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));

@@ -33,6 +33,14 @@
 #endif
 #define SP_RNG_PF SP_CHUNK_RNG_PF
 #define SP_RHO_TOUCH 1
+// The generator store is written generation after generation by ck_count's twists and read by
+// ck_shade at each chunk's position: word-interleaved rows measured best here (8-way shard 2785-2790
+// Mrays/s per GPU against 2745-2765 with 4-word lane blocks; profiles/r04/rng_layout).
+#ifndef SP_CHUNK_MT_BLK
+#define SP_CHUNK_MT_BLK 1
+#endif
+#undef SP_MT_BLK
+#define SP_MT_BLK SP_CHUNK_MT_BLK
 #include "sp_chunk.hpp"
 
 #include <cstdlib>
@@ -178,7 +186,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
         if (slot >= a.num_tiles) break;
         const Px     px = pixel(sc, a, slot, lane);
         const size_t p  = (size_t)slot * 64 + lane;
-        rng.base        = a.gens + (size_t)slot * a.gens_per_px * (MT_N * 64) + lane;
+        rng.base        = a.gens + (size_t)slot * a.gens_per_px * MT_GEN_WORDS + (size_t)lane * MT_BLK;
         if (px.inside) rng_seed(rng, ((px.x << 16u) | px.y) ^ 0xb0ae9d99u); // main.cpp:73
         if (a.draws) {
             // Counts known from the camera pass: the stream position before sample i is the sum
@@ -265,7 +273,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) ck_shade(Scene sc,
         if (px.inside && i0 < i1) {
         // every generation this chunk draws from was written by ck_count: read-only stream
         const uint32_t st = a.snap_ctl[(size_t)c * a.n_px + p];
-        rng.base  = a.gens + (size_t)slot * a.gens_per_px * (MT_N * 64) + lane;
+        rng.base  = a.gens + (size_t)slot * a.gens_per_px * MT_GEN_WORDS + (size_t)lane * MT_BLK;
         rng.idx   = (int)(st & 0xffffu);
         rng.cur   = (int)(st >> 16);
         rng.lin   = 1;

@@ -133,6 +133,26 @@ struct Scene {
 // spilled to VGPR lanes and read back with v_readlane in every sample of the rho loop (elf
 // 1024^2 @ 16 spp 571-586 -> 600-603 Mrays/s, bunny +1 %, profiles/r03).
 constexpr int RSQ_HDR = 8;
+
+// Device layout of the std::mt19937_64 states (main.cpp:73: one per pixel; 312 words per
+// generation).  A wave slot holds 64 lanes' states; word k of lane l of one generation buffer is at
+// (k / MT_BLK) * 64 * MT_BLK + l * MT_BLK + k % MT_BLK: each lane's MT_BLK consecutive words share
+// one 128-byte line.  A lane draws its words in order, and the served estimates of IterativeRRNEE
+// read 32 consecutive words of another lane's stream, while the lanes' stream positions drift
+// apart after the first sample; with the words interleaved by lane (MT_BLK = 1, rounds 1-3) every
+// draw touched its own line -- elf's 8-way shard fetched 39.7 TB per frame for ~7 TB of state
+// reads (profiles/r04/traffic).  A twist (all lanes, word by word) now reuses each lane's line
+// for MT_BLK consecutive words from L1/L2.  Buffers are padded to whole blocks.
+#ifndef SP_MT_BLK
+#define SP_MT_BLK 4
+#endif
+constexpr int MT_BLK       = SP_MT_BLK;
+// no padding: every translation unit sizes a generation buffer the same (the sample-chunk TU keeps
+// its own block size for its generator store, sp_chunk.hip)
+static_assert(spm::MT_N % MT_BLK == 0, "MT_BLK must divide 312");
+constexpr int MT_ROWS      = (spm::MT_N + MT_BLK - 1) / MT_BLK;
+constexpr int MT_GEN_WORDS = MT_ROWS * MT_BLK * 64; // words of one generation buffer of a wave slot
+__host__ __device__ inline size_t mt_off(int k) { return (size_t)(k / MT_BLK) * (64 * MT_BLK) + (size_t)(k % MT_BLK); }
 __host__ __device__ inline int rsqrt_words(const Scene& sc) { return RSQ_HDR + (sc.rsqrt_shift ? (1 << sc.rsqrt_bits) : (2 << sc.rsqrt_bits)); }
 
 

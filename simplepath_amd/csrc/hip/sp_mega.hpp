@@ -46,7 +46,7 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
 
     const size_t gwave = (size_t)blockIdx.x * WAVES_PER_BLOCK + wave;
     Rng          rng;
-    rng.base = args.mt_state + gwave * (2 * MT_N * 64) + lane;
+    rng.base = args.mt_state + gwave * (2 * (size_t)MT_GEN_WORDS) + (size_t)lane * MT_BLK;
 
     uint32_t rays_total = 0, shadow_total = 0, samples_total = 0, draws_total = 0;
     const uint32_t dx = morton_decode_1((uint32_t)lane);

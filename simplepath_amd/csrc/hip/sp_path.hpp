@@ -101,7 +101,7 @@ __device__ __forceinline__ float sqrt_unit(float x)
 #endif
 constexpr int RNG_PF = SP_RNG_PF;
 struct Rng {
-    uint64_t* base;  // lane-offset base of this wave slot's state, stride 64 words
+    uint64_t* base;  // this lane's base in its wave slot's state (sp_device.hpp mt_off layout)
     int       cur;   // generation buffer being consumed
     int       idx;   // next word in it
     int       ready; // other buffer already holds the next generation
@@ -125,7 +125,7 @@ struct Rng {
 #endif
 };
 
-__device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_N * 64; }
+__device__ __forceinline__ uint64_t* mt_buf(Rng& r, int b) { return r.base + (size_t)b * MT_GEN_WORDS; }
 __device__ __forceinline__ int       mt_next(const Rng& r) { return r.lin ? r.cur + 1 : r.cur ^ 1; }
 
 // B = twist(A) without modifying A (in-place MT19937-64 twist split over two buffers), for twists
@@ -151,12 +151,12 @@ __device__ __forceinline__ void mt_twist_words(const uint64_t* __restrict__ A, u
         uint64_t a1[NW], am[NW];
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
-            a1[j] = A[(k + j + 1) * 64];
-            am[j] = SECOND ? B[(k + j - (MT_N - MT_M)) * 64] : A[(k + j + MT_M) * 64];
+            a1[j] = A[mt_off(k + j + 1)];
+            am[j] = SECOND ? B[mt_off(k + j - (MT_N - MT_M))] : A[mt_off(k + j + MT_M)];
         }
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
-            B[(k + j) * 64] = am[j] ^ mt_mix(ak, a1[j]);
+            B[mt_off(k + j)] = am[j] ^ mt_mix(ak, a1[j]);
             ak              = a1[j];
         }
     }
@@ -173,7 +173,7 @@ __device__ __forceinline__ void mt_twist_blocked(const uint64_t* __restrict__ A,
 #pragma unroll 1
     for (int b = 0; b < N2 / U; ++b) mt_twist_words<U, true>(A, B, H + b * U, ak);
     mt_twist_words<N2 % U, true>(A, B, H + (N2 / U) * U, ak);
-    B[(MT_N - 1) * 64] = B[(MT_M - 1) * 64] ^ mt_mix(ak, B[0]);
+    B[mt_off(MT_N - 1)] = B[mt_off(MT_M - 1)] ^ mt_mix(ak, B[0]);
 }
 
 // B = twist(A) without modifying A: the compact form, for twists inside register-heavy code (the
@@ -184,17 +184,17 @@ __device__ __forceinline__ void mt_twist_into(const uint64_t* A, uint64_t* B)
     uint64_t ak = A[0];
 #pragma unroll 4
     for (int k = 0; k < MT_N - MT_M; ++k) {
-        const uint64_t ak1 = A[(k + 1) * 64];
-        B[k * 64]          = A[(k + MT_M) * 64] ^ mt_mix(ak, ak1);
+        const uint64_t ak1 = A[mt_off(k + 1)];
+        B[mt_off(k)]       = A[mt_off(k + MT_M)] ^ mt_mix(ak, ak1);
         ak                 = ak1;
     }
 #pragma unroll 4
     for (int k = MT_N - MT_M; k < MT_N - 1; ++k) {
-        const uint64_t ak1 = A[(k + 1) * 64];
-        B[k * 64]          = B[(k - (MT_N - MT_M)) * 64] ^ mt_mix(ak, ak1);
+        const uint64_t ak1 = A[mt_off(k + 1)];
+        B[mt_off(k)]       = B[mt_off(k - (MT_N - MT_M))] ^ mt_mix(ak, ak1);
         ak                 = ak1;
     }
-    B[(MT_N - 1) * 64] = B[(MT_M - 1) * 64] ^ mt_mix(ak, B[0]);
+    B[mt_off(MT_N - 1)] = B[mt_off(MT_M - 1)] ^ mt_mix(ak, B[0]);
 }
 
 __device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
@@ -204,7 +204,7 @@ __device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
     b[0]        = x;
     for (int i = 1; i < MT_N; ++i) {
         x          = mt_seed_next(x, (uint64_t)i);
-        b[i * 64]  = x;
+        b[mt_off(i)] = x;
     }
     r.cur   = 0;
     r.idx   = MT_N; // std::mt19937_64 starts with _M_p = n: first draw twists
@@ -253,14 +253,14 @@ __device__ __forceinline__ uint64_t rng_raw(Rng& r)
         for (int k = 0; k + 1 < RNG_PF; ++k) r.pf[k] = r.pf[k + 1];
         --r.pfn;
     } else {
-        w = b[(size_t)r.idx * 64];
+        w = b[mt_off(r.idx)];
     }
     ++r.idx;
     // top the window up to RNG_PF words ahead (static indices: the window stays in registers)
 #pragma unroll
     for (int k = 0; k < RNG_PF; ++k)
         if (r.pfn == k && r.idx + k < MT_N) {
-            r.pf[k] = b[(size_t)(r.idx + k) * 64];
+            r.pf[k] = b[mt_off(r.idx + k)];
             r.pfn   = k + 1;
         }
     ++r.draws;
@@ -311,13 +311,22 @@ __device__ __forceinline__ void rng_skip_reserved(Rng& r, int n)
 // touched in the next buffer only when it already holds the next generation.
 __device__ __forceinline__ void rng_touch(const Rng& r, int n, __attribute__((address_space(3))) void* sink)
 {
-    const uint64_t* cur  = r.base + (size_t)r.cur * MT_N * 64;
-    const uint64_t* next = r.base + (size_t)mt_next(r) * MT_N * 64;
+    const uint64_t* cur  = r.base + (size_t)r.cur * MT_GEN_WORDS;
+    const uint64_t* next = r.base + (size_t)mt_next(r) * MT_GEN_WORDS;
+    if constexpr (MT_BLK == 1) {
 #pragma unroll 4
-    for (int k = 0; k < n; ++k) {
-        const int row = r.idx + k;
-        if (row < MT_N) __builtin_amdgcn_global_load_lds((const void*)(cur + (size_t)row * 64), sink, 4, 0, 0);
-        else if (r.ready) __builtin_amdgcn_global_load_lds((const void*)(next + (size_t)(row - MT_N) * 64), sink, 4, 0, 0);
+        for (int k = 0; k < n; ++k) {
+            const int row = r.idx + k;
+            if (row < MT_N) __builtin_amdgcn_global_load_lds((const void*)(cur + mt_off(row)), sink, 4, 0, 0);
+            else if (r.ready) __builtin_amdgcn_global_load_lds((const void*)(next + mt_off(row - MT_N)), sink, 4, 0, 0);
+        }
+    } else { // one touch per line: words idx .. idx + n - 1 of this generation, the rest of the next
+        const int end = r.idx + n;
+        for (int row = r.idx; row < end && row < MT_N; row = (row / MT_BLK + 1) * MT_BLK)
+            __builtin_amdgcn_global_load_lds((const void*)(cur + mt_off(row)), sink, 4, 0, 0);
+        if (r.ready)
+            for (int row = 0; row < end - MT_N; row += MT_BLK)
+                __builtin_amdgcn_global_load_lds((const void*)(next + mt_off(row)), sink, 4, 0, 0);
     }
 }
 
@@ -2594,7 +2603,7 @@ __device__ __forceinline__ void serve_rho(Ctx& c, bool want, bool want_a, int mi
                 idx -= MT_N;
             }
             float w[2];
-            served_weights(c.sc.materials[obase], owo, c.rng.base - lane + o, cur, idx, c.q, w);
+            served_weights(c.sc.materials[obase], owo, c.rng.base + (o - lane) * MT_BLK, cur, idx, c.q, w);
             srv_w_at(wave, k, 0)[o] = w[0];
             srv_w_at(wave, k, 1)[o] = w[1];
         }

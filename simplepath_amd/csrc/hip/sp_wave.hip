@@ -143,7 +143,7 @@ __device__ __forceinline__ Rng rng_load(const WaveArgs& w, int64_t p)
 {
     Rng            r;
     const uint32_t st = w.rstate[p];
-    r.base  = w.mt_state + (size_t)(p >> 6) * (2 * MT_N * 64) + (p & 63);
+    r.base  = w.mt_state + (size_t)(p >> 6) * (2 * (size_t)MT_GEN_WORDS) + (size_t)(p & 63) * MT_BLK;
     r.idx   = (int)(st & 0xffffu);
     r.cur   = (int)((st >> 16) & 1u);
     r.ready = (int)((st >> 17) & 1u);
@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(WF_BLOCK) wf_init(Scene sc, WaveArgs w)
         return;
     }
     Rng r;
-    r.base = w.mt_state + (size_t)(p >> 6) * (2 * MT_N * 64) + (p & 63);
+    r.base = w.mt_state + (size_t)(p >> 6) * (2 * (size_t)MT_GEN_WORDS) + (size_t)(p & 63) * MT_BLK;
     rng_seed(r, ((pr.px << 16u) | pr.py) ^ 0xb0ae9d99u); // get_integrator_sampler (main.cpp:73)
     rng_store(w, p, r);
 }
@@ -440,7 +440,7 @@ static uint32_t diag_sample_env()
 
 size_t wave_bytes_per_pixel(int n_lights)
 {
-    return 3 * 4 + 4 + 16 + 16 + (size_t)n_lights * 32 + 4 + 2 * MT_N * 8;
+    return 3 * 4 + 4 + 16 + 16 + (size_t)n_lights * 32 + 4 + 2 * (size_t)(MT_GEN_WORDS / 64) * 8;
 }
 // primary/shade/resolve slots (one per tile) + persistent shadow-wave slots (at most as many)
 // tile slots + persistent shadow-wave slots of both parts (each part's grid is at most

@@ -219,3 +219,14 @@ def test_one_scene_two_threads_two_streams(scene_dir, integrator):
     assert not errors, errors
     for k in range(2):
         assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), refs[k].view(np.uint32)), k
+
+
+def test_scene_device_bytes(scene_dir):
+    # sp_scene_device_bytes: the resident scene's HBM bytes (bench.py counts them in the
+    # algorithmic bytes of a frame); at least the triangle records of both BVH layouts
+    s = load(scene_dir, "bunny.sp", 64, 40)
+    info = s.bvh_info()
+    b = s.device_bytes()
+    assert b >= 2 * info["slots"] * 48 and b < 200e6
+    s.upload(device=0, bvh_mode=1)  # the reference BVH alone: no 8-wide copy
+    assert 0 < s.device_bytes() < b
