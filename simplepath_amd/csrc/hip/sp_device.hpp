@@ -11,6 +11,7 @@
 #pragma once
 #include "../common/sp_libm.h"
 #include "../common/sp_rng.h"
+#include "../common/sp_twist4.h"
 #include "../../../include/simplepath_hip.h"
 
 namespace spd {

@@ -164,6 +164,13 @@ __device__ __forceinline__ void mt_twist_words(const uint64_t* __restrict__ A, u
 template <int U>
 __device__ __forceinline__ void mt_twist_blocked(const uint64_t* __restrict__ A, uint64_t* __restrict__ B)
 {
+#ifndef SP_TWIST_GROUPED
+#define SP_TWIST_GROUPED 1
+#endif
+    if constexpr (MT_BLK == 4 && SP_TWIST_GROUPED) { // 4-word lane groups, 3 per block (sp_twist4.h)
+        mt_twist_grouped4<3>(A, B);
+        return;
+    }
     constexpr int H  = MT_N - MT_M;     // words 0 .. H - 1 mix with A[k + M]
     constexpr int N2 = MT_N - 1 - H;    // words H .. N - 2 mix with B[k - H]
     uint64_t      ak = A[0];

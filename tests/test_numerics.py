@@ -122,3 +122,17 @@ def test_rsqrt_table_override_concurrent_readers(scene_dir):
         stop.set()
         th.join()
         sp.set_rsqrt_table(None)
+
+
+def test_grouped_twist_matches_libstdcxx(tmp_path):
+    # the device's 4-word grouped twist (sp_twist4.h, used with the lane-blocked state layout)
+    # compiled for the host: 5 consecutive generations x 3 seeds x 4 lane positions, every word
+    # against std::mt19937_64 itself
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "twist4_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "simplepath_amd", "csrc", "common"),
+                    os.path.join(root, "tests", "cpp", "twist4_check.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatching" in r.stdout

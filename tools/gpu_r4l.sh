@@ -6,7 +6,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not bench_ranks" > gpurun_out/r4l_tests.log 2>&1 || { tail -30 gpurun_out/r4l_tests.log; exit 1; }
 tail -1 gpurun_out/r4l_tests.log
 for r in 1 2; do
-for b in _build _build_b2 _build_b8; do
+for b in _build _build_b4w _build_b2 _build_b8; do
   L=$PWD/simplepath_amd/$b/libsimplepath_hip.so
   SP_LIB_PATH=$L timeout -k 10 200 python bench.py --no-cpu > gpurun_out/ab.json 2>/dev/null || exit 1
   echo "bunny $b: $(python -c "import json;d=json.load(open('gpurun_out/ab.json'));print(d['value'], d['ms_per_step'])")"
