@@ -49,6 +49,10 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
     rng.base = args.mt_state + gwave * (2 * (size_t)MT_GEN_WORDS) + (size_t)lane * MT_BLK;
 
     uint32_t rays_total = 0, shadow_total = 0, samples_total = 0, draws_total = 0;
+    // The probe's tile times are timer readings (run-to-run noise) and only order the queue, so
+    // its draws need not be the pixels' own streams: each lane seeds once and its stream runs on
+    // across the wave's tiles, instead of a 312-word seed and a first twist per tile.
+    if constexpr (PROBE) rng_seed(rng, (uint32_t)(gwave * 64 + lane) ^ 0xb0ae9d99u);
     const uint32_t dx = morton_decode_1((uint32_t)lane);
     const uint32_t dy = morton_decode_1((uint32_t)lane >> 1);
     while (true) {
@@ -67,7 +71,10 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
         uint64_t       prof[4] = { 0, 0, 0, 0 };
         if (inside) {
             const uint32_t pix_seed = (px << 16u) | py;
-            rng_seed(rng, pix_seed ^ 0xb0ae9d99u);          // get_integrator_sampler (main.cpp:73)
+            if constexpr (!PROBE) { // get_integrator_sampler (main.cpp:73)
+                if (SP_SEED_FUSED) rng_seed_twisted(rng, pix_seed ^ 0xb0ae9d99u);
+                else rng_seed(rng, pix_seed ^ 0xb0ae9d99u);
+            }
             const uint32_t seed2d = pix_seed ^ 0x6184faf4u; // RSequenceSampler m_seed_2D (main.cpp:67)
             Ctx c{ sc, rng, q, st, 0u, 0u };
             if (args.deep) {

@@ -220,6 +220,56 @@ __device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
     r.pfn   = 0;
 }
 
+// rng_seed followed by the first twist, without storing or re-reading the seeded state: the engine
+// starts with _M_p = n, so the seeded words are only ever read by that twist.  Generation 1 goes
+// straight into the next buffer: word k < M mixes seeded words k, k + 1 and k + M, taken from two
+// running seed chains (the second started M steps ahead); word k in [M, N - 1) mixes seeded words
+// k, k + 1 with the new word k - M, written M words before (read back in blocks of 12, all loads of
+// a block issued before its stores).  The same state as rng_seed + mt_twist_blocked (cur = 0 at
+// its end, next buffer ready).
+#ifndef SP_SEED_FUSED
+#define SP_SEED_FUSED 1
+#endif
+__device__ __forceinline__ void rng_seed_twisted(Rng& r, uint32_t seed)
+{
+    static_assert(MT_N - MT_M == MT_M, "two seed chains M apart cover words 0 .. N - 1");
+    r.cur         = 0;
+    uint64_t*  B  = mt_buf(r, mt_next(r));
+    uint64_t   xk = (uint64_t)seed, xm = (uint64_t)seed;
+#pragma unroll 4
+    for (int i = 1; i <= MT_M; ++i) xm = mt_seed_next(xm, (uint64_t)i);
+    uint64_t b0 = 0;
+#pragma unroll 4
+    for (int k = 0; k < MT_M; ++k) {
+        const uint64_t xk1 = mt_seed_next(xk, (uint64_t)(k + 1));
+        const uint64_t w   = xm ^ mt_mix(xk, xk1);
+        B[mt_off(k)]       = w;
+        if (k == 0) b0 = w;
+        xm = mt_seed_next(xm, (uint64_t)(k + MT_M + 1));
+        xk = xk1;
+    }
+    constexpr int U = 12, NW = MT_N - 1 - MT_M; // words M .. N - 2
+#pragma unroll 1
+    for (int k0 = MT_M; k0 < MT_M + NW; k0 += U) {
+        uint64_t p[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+            if (k0 + j < MT_M + NW) p[j] = B[mt_off(k0 + j - MT_M)];
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+            if (k0 + j < MT_M + NW) {
+                const uint64_t xk1 = mt_seed_next(xk, (uint64_t)(k0 + j + 1));
+                B[mt_off(k0 + j)]  = p[j] ^ mt_mix(xk, xk1);
+                xk                 = xk1;
+            }
+    }
+    B[mt_off(MT_N - 1)] = B[mt_off(MT_M - 1)] ^ mt_mix(xk, b0);
+    r.idx   = MT_N;
+    r.ready = 1;
+    r.draws = 0;
+    r.pfn   = 0;
+}
+
 // Twist ahead at a wave-synchronous point (sample / bounce start).  A lane may compute its next
 // generation any time after starting the current one, so all lanes whose next buffer is stale
 // twist together -- but only once some lane is within RNG_MARGIN draws of exhausting its buffer.
