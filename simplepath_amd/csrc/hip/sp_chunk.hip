@@ -187,7 +187,9 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
         const Px     px = pixel(sc, a, slot, lane);
         const size_t p  = (size_t)slot * 64 + lane;
         rng.base        = a.gens + (size_t)slot * a.gens_per_px * MT_GEN_WORDS + (size_t)lane * MT_BLK;
-        if (px.inside) rng_seed(rng, ((px.x << 16u) | px.y) ^ 0xb0ae9d99u); // main.cpp:73
+        // main.cpp:73; generation 0 (the seeded state) is never drawn from, so it is not stored:
+        // the seed writes generation 1 (rng_seed_twisted), the replay twists on from there
+        if (px.inside) rng_seed_twisted(rng, ((px.x << 16u) | px.y) ^ 0xb0ae9d99u);
         if (a.draws) {
             // Counts known from the camera pass: the stream position before sample i is the sum
             // of the earlier counts, so the counts are summed in batches of loads that are all in
@@ -215,7 +217,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_count(Scene sc, Chunk
             if (px.inside) {
                 const uint32_t G = T ? (T - 1) / MT_N + 1 : 0u;
 #pragma unroll 1
-                for (uint32_t g = 0; g < G; ++g) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(rng, (int)g), mt_buf(rng, (int)g + 1));
+                for (uint32_t g = 1; g < G; ++g) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(rng, (int)g), mt_buf(rng, (int)g + 1));
             }
             continue;
         }
