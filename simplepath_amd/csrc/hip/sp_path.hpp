@@ -1867,13 +1867,22 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     // the final erfinv is only evaluated when the loop ran out of iterations (b moved after it)
     float inv_erf   = 0.0f;
     bool  converged = false;
+#if defined(SP_WAVE_PROF) && defined(SP_WPROF_NEWTON) // regions 4 / 5: each iteration / the whole loop
+    const uint64_t t_nl = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll 1 // data-dependent exit: unrolled copies only grow the hot loop
     for (int it = 0; it < 9; ++it) {
+#if defined(SP_WAVE_PROF) && defined(SP_WPROF_NEWTON)
+        const uint64_t t_it = __builtin_amdgcn_s_memtime();
+#endif
         if (!(b >= a && b <= c)) b = 0.5f * (a + c);
         inv_erf = erfinv(b);
         const float value =
             p.normalization * (1.0f + b + p.sqrt_pi_inv * p.tan_theta_i * lm_expf(-inv_erf * inv_erf)) - sample_x;
         const float derivative = p.normalization * (1.0f - inv_erf * p.tan_theta_i);
+#if defined(SP_WAVE_PROF) && defined(SP_WPROF_NEWTON)
+        wprof_end(4, t_it);
+#endif
         if (abs_f(value) < 1e-5f) {
             converged = true;
             break;
@@ -1882,6 +1891,9 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
         else a = b;
         b -= value / derivative;
     }
+#if defined(SP_WAVE_PROF) && defined(SP_WPROF_NEWTON)
+    wprof_end(5, t_nl);
+#endif
     s.x = converged ? inv_erf : erfinv(b);
     s.y = erfinv(2.0f * std_max(U2, 1e-6f) - 1.0f);
     return s;
