@@ -209,9 +209,10 @@ typedef struct sp_render_params {
                                          the buffers do not fit                                    */
     /* ---- ABI 5 ---- */
     float          tile_order_factor; /* megakernel tile order (DirectLighting, IterativeRRNEE): 0 =
-                                         automatic (a one-sample probe times every tile and tiles
-                                         slower than 2x the mean go first, from 6 tiles per wave and
-                                         128 spp); > 0: always, with this factor; < 0: queue order  */
+                                         automatic (a one-sample probe times every tile; tiles
+                                         slower than 2x the mean go first, then those slower than
+                                         1x, 0.5x, ... the mean; from 6 tiles per wave and 128 spp);
+                                         > 0: always, with this factor; < 0: queue order            */
     int32_t        reserved[2];       /* must be 0                                                  */
 } sp_render_params;
 

@@ -1340,7 +1340,10 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             }
             if (!s->probe_counters) SP_HIP(hipMalloc(&s->probe_counters, 8 * sizeof(unsigned long long)));
             spd::RenderArgs pr = a;
-            pr.spp       = 1; // 2 or 4 probe samples measured no better (profiles/r03/ab_tile_order.txt)
+#ifndef SP_PROBE_SPP
+#define SP_PROBE_SPP 1
+#endif
+            pr.spp       = SP_PROBE_SPP; // 2 or 4 probe samples measured no better (profiles/r03/ab_tile_order.txt)
             pr.tile_time = s->d_tile_time;
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
