@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront", "chunks"])
     ap.add_argument("--waves", type=int, default=0,
                     help="megakernel occupancy variant (sp_render_params.waves_per_simd; 0 = automatic)")
+    ap.add_argument("--tile-order-factor", type=float, default=0.0,
+                    help="megakernel tile order (sp_render_params.tile_order_factor): 0 automatic, > 0 always, < 0 queue order")
     ap.add_argument("--per-lane-queries", action="store_true",
                     help="IterativeRRNEE: walk every ray on its own lane (SP_RENDER_PER_LANE_QUERIES; comparison)")
     ap.add_argument("--sim-world", type=int, default=0,
@@ -248,7 +250,7 @@ def main():
             return _CpuStats(st, (time.perf_counter() - t) * 1e3)
         return sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
                                       pipeline=args.pipeline, stage_timing=True, waves_per_simd=args.waves,
-                                      per_lane_queries=args.per_lane_queries)
+                                      per_lane_queries=args.per_lane_queries, tile_order_factor=args.tile_order_factor)
 
     def step():
         st = render()

@@ -211,7 +211,8 @@ typedef struct sp_render_params {
     float          tile_order_factor; /* megakernel tile order (DirectLighting, IterativeRRNEE): 0 =
                                          automatic (a one-sample probe times every tile; tiles
                                          slower than 2x the mean go first, then those slower than
-                                         1x, 0.5x, ... the mean; from 6 tiles per wave and 128 spp);
+                                         1x, 0.5x, ... the mean; from 6 tiles per wave and 128 spp,
+                                         IterativeRRNEE from 4 tiles per wave and 16 spp);
                                          > 0: always, with this factor; < 0: queue order            */
     int32_t        reserved[2];       /* must be 0                                                  */
 } sp_render_params;

@@ -1316,16 +1316,18 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         a.order     = nullptr;
         a.tile_time = nullptr;
         // Tile order (sp_mega.hip tile_order): a one-sample probe pass times every tile, and the
-        // tiles slower than `hoist` x the mean go to the front of the queue, so the frame does not
-        // end with a few waves finishing expensive tiles alone.  Part of the render (timed with
-        // it); stream-ordered, no host wait.  Used where it measured faster (profiles/r03/
-        // ab_tile_order.txt): many tiles per persistent wave and a probe that costs little of the
-        // frame -- bunny 1080p @ 256 spp (7.9 tiles per wave) +3-4 %, lucy +2 %, elf's 8-way
-        // shard +3 %; spheres 1024^2 (4 tiles per wave) lost 1 % at 256 spp and 5 % at 64 spp.
-        // DirectLighting and IterativeRRNEE have probe kernels (sp_probe_*.hip); the other
-        // integrators render in queue order.  sp_render_params.tile_order_factor > 0 forces it with
-        // that factor, < 0 turns it off.
-        float hoist = (n_tiles >= 6 * (int64_t)waves && p->samples_per_pixel >= 128) ? 2.0f : 0.0f;
+        // queue is ordered by cost class (slower than `hoist` x the mean first, the cheapest last),
+        // so the frame does not end with a few waves finishing expensive tiles alone.  Part of the
+        // render (timed with it); stream-ordered, no host wait.  Used where it measured faster
+        // (profiles/r03/ab_tile_order.txt, profiles/r04/tile_classes/): DirectLighting with many
+        // tiles per persistent wave and a probe that costs little of the frame (bunny 1080p @ 256
+        // spp, 7.9 tiles per wave; lucy; spheres 1024^2 @ 64 spp, 4 tiles per wave, loses 1 %);
+        // IterativeRRNEE, whose tile costs spread wider (paths end at any depth), from 4 tiles per
+        // wave and 16 spp (elf 1024^2 @ 16 spp +1.7 %; elf's 8-way shard +3 % with two classes, +5 % more with six).  DirectLighting and
+        // IterativeRRNEE have probe kernels (sp_probe_*.hip); the other integrators render in queue
+        // order.  sp_render_params.tile_order_factor > 0 forces it with that factor, < 0 turns it off.
+        const bool rrnee = integ == SP_INTEGRATOR_ITERATIVE_RRNEE;
+        float      hoist = (n_tiles >= (rrnee ? 4 : 6) * (int64_t)waves && p->samples_per_pixel >= (rrnee ? 16u : 128u)) ? 2.0f : 0.0f;
         if (p->tile_order_factor != 0.0f) hoist = std::max(0.0f, p->tile_order_factor);
         if (hoist > 0.0f && n_tiles > (int64_t)waves && spd::has_probe(integ)) {
             if ((size_t)n_tiles > s->order_cap) {
@@ -1340,10 +1342,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             }
             if (!s->probe_counters) SP_HIP(hipMalloc(&s->probe_counters, 8 * sizeof(unsigned long long)));
             spd::RenderArgs pr = a;
-#ifndef SP_PROBE_SPP
-#define SP_PROBE_SPP 1
-#endif
-            pr.spp       = SP_PROBE_SPP; // 2 or 4 probe samples measured no better (profiles/r03/ab_tile_order.txt)
+            pr.spp       = 1; // 2 or 4 probe samples measured no better (profiles/r03/ab_tile_order.txt, r04/tile_classes)
             pr.tile_time = s->d_tile_time;
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
