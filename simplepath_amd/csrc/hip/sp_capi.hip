@@ -1244,7 +1244,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         a.out         = d_out;
         SP_HIP(hipMemsetAsync(s->ck_ctr, 0, 2 * sizeof(int32_t), stream));
         SP_HIP(hipEventRecord(s->ev0, stream));
-        SP_HIP(spd::chunk_render(s->dev, a, blocks, stream));
+        SP_HIP(spd::chunk_render(s->dev, a, blocks, s->n_cu, stream));
         launches = 4;
     } else {
         const int    rs_words  = spd::rsqrt_words(s->dev);

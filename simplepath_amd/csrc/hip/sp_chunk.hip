@@ -43,6 +43,7 @@
 #define SP_MT_BLK SP_CHUNK_MT_BLK
 #include "sp_chunk.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include "sp_mega.hpp"
 
@@ -139,13 +140,11 @@ __device__ __forceinline__ uint32_t sample_draws(const Scene& sc, const Isect& i
 } // namespace
 
 // ---------------------------------------------------------------------------- camera rays
-__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_camera(Scene sc, ChunkArgs a)
+// Persistent: each wave takes items (tile, sample) w, w + W, w + 2W, ... (W = the grid's waves), so
+// the LDS tables are loaded once per block instead of once per 64 camera rays (one block per item
+// group used to load the RSQRTSS table and libm tables for 4 x 64 rays).
+__device__ __forceinline__ void camera_item(const Scene& sc, const ChunkArgs& a, const Lds& l, uint32_t lane, int64_t item)
 {
-    extern __shared__ uint32_t lds[];
-    const Lds      l    = lds_setup(sc, lds, true);
-    const uint32_t lane = threadIdx.x & 63u;
-    const int64_t  item = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    if (item >= a.num_tiles * (int64_t)a.spp) return;
     const int64_t  slot = item % a.num_tiles;
     const uint32_t i    = (uint32_t)(item / a.num_tiles);
     const Px       px   = pixel(sc, a, slot, lane);
@@ -170,6 +169,16 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_camera(Scene sc, Chun
     a.L[((size_t)i * 3 + 0) * a.n_px + p] = L.r;
     a.L[((size_t)i * 3 + 1) * a.n_px + p] = L.g;
     a.L[((size_t)i * 3 + 2) * a.n_px + p] = L.b;
+}
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK) ck_camera(Scene sc, ChunkArgs a)
+{
+    extern __shared__ uint32_t lds[];
+    const Lds      l     = lds_setup(sc, lds, true);
+    const uint32_t lane  = threadIdx.x & 63u;
+    const int64_t  total = a.num_tiles * (int64_t)a.spp;
+    const int64_t  W     = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    for (int64_t item = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6); item < total; item += W)
+        camera_item(sc, a, l, lane, item);
 }
 
 // ------------------------------------------------------------------- stream positions (replay)
@@ -336,13 +345,18 @@ int chunk_blocks_per_cu(size_t lds_bytes)
     return n > 0 ? n : 1;
 }
 
-hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, hipStream_t stream)
+hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int n_cu, hipStream_t stream)
 {
     const size_t rs_bytes    = (size_t)rsqrt_words(sc) * 4;
     const size_t stack_bytes = (size_t)WAVES_PER_BLOCK * sc.stack_words * 64 * 4;
     const int64_t cam_waves  = a.num_tiles * (int64_t)a.spp;
-    hipLaunchKernelGGL(ck_camera, dim3((unsigned)((cam_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
-                       dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes, stream, sc, a);
+    int           cam_per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&cam_per_cu, ck_camera, 64 * WAVES_PER_BLOCK, rs_bytes + stack_bytes) !=
+            hipSuccess || cam_per_cu < 1)
+        cam_per_cu = 1;
+    const int64_t cam_blocks = std::max<int64_t>(1, std::min<int64_t>((cam_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK,
+                                                                      (int64_t)cam_per_cu * std::max(1, n_cu)));
+    hipLaunchKernelGGL(ck_camera, dim3((unsigned)cam_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes, stream, sc, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ck_count, dim3((unsigned)((a.num_tiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),

@@ -27,6 +27,6 @@ struct ChunkArgs {
 };
 
 int        chunk_blocks_per_cu(size_t lds_bytes);
-hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, hipStream_t stream);
+hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int n_cu, hipStream_t stream);
 
 } // namespace spd
