@@ -161,6 +161,13 @@ __device__ __forceinline__ void mt_twist_words(const uint64_t* __restrict__ A, u
         }
     }
 }
+struct MtOff {
+    __device__ __forceinline__ size_t operator()(int k) const { return mt_off(k); }
+};
+// SP_TWIST_FUSED: the one-pass forms of sp_twist4.h (every word of A loaded once, B not read back)
+#ifndef SP_TWIST_FUSED
+#define SP_TWIST_FUSED 1
+#endif
 template <int U>
 __device__ __forceinline__ void mt_twist_blocked(const uint64_t* __restrict__ A, uint64_t* __restrict__ B)
 {
@@ -168,7 +175,12 @@ __device__ __forceinline__ void mt_twist_blocked(const uint64_t* __restrict__ A,
 #define SP_TWIST_GROUPED 1
 #endif
     if constexpr (MT_BLK == 4 && SP_TWIST_GROUPED) { // 4-word lane groups, 3 per block (sp_twist4.h)
-        mt_twist_grouped4<3>(A, B);
+        if (SP_TWIST_FUSED) mt_twist_grouped4_fused<3>(A, B);
+        else mt_twist_grouped4<3>(A, B);
+        return;
+    }
+    if constexpr (SP_TWIST_FUSED) {
+        mt_twist_fused<U>(A, B, MtOff{});
         return;
     }
     constexpr int H  = MT_N - MT_M;     // words 0 .. H - 1 mix with A[k + M]
