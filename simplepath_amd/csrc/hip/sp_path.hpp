@@ -198,8 +198,15 @@ __device__ __forceinline__ void mt_twist_blocked(const uint64_t* __restrict__ A,
 // B = twist(A) without modifying A: the compact form, for twists inside register-heavy code (the
 // in-draw fallback, rng_reserve), where the blocked form's 4 x SP_TWIST_BLOCK live registers would
 // spill.
+#ifndef SP_TWIST_INTO_FUSED
+#define SP_TWIST_INTO_FUSED 0
+#endif
 __device__ __forceinline__ void mt_twist_into(const uint64_t* A, uint64_t* B)
 {
+    if constexpr (SP_TWIST_INTO_FUSED > 0) { // one pass, SP_TWIST_INTO_FUSED words per block of loads
+        mt_twist_fused<SP_TWIST_INTO_FUSED>(A, B, MtOff{});
+        return;
+    }
     uint64_t ak = A[0];
 #pragma unroll 4
     for (int k = 0; k < MT_N - MT_M; ++k) {
