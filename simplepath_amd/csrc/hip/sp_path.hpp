@@ -140,8 +140,8 @@ __device__ __forceinline__ int       mt_next(const Rng& r) { return r.lin ? r.cu
 #ifndef SP_TWIST_BLOCK
 #define SP_TWIST_BLOCK 12
 #endif
-#ifndef SP_TWIST_SKIP_BLOCK
-#define SP_TWIST_SKIP_BLOCK 24
+#ifndef SP_TWIST_SKIP_BLOCK // 12 since the one-pass twist (2-way shard +0.9 %, 8-way level: profiles/r04/rng_layout/ab_skip_block.txt)
+#define SP_TWIST_SKIP_BLOCK 12
 #endif
 // words k .. k + NW - 1 of B; the words mixed in come from A[k + M] (first part) or B[k - (N - M)]
 template <int NW, bool SECOND>
