@@ -213,7 +213,15 @@ typedef struct sp_render_params {
                                          slower than 2x the mean go first, then those slower than
                                          1x, 0.5x, ... the mean; from 6 tiles per wave and 128 spp,
                                          IterativeRRNEE from 4 tiles per wave and 16 spp);
-                                         > 0: always, with this factor; < 0: queue order            */
+                                         > 0: with this factor whenever it can apply; < 0: queue
+                                         order.  It cannot apply, and the frame renders in queue
+                                         order whatever the factor, when the megakernel does not
+                                         run (wavefront, sample chunks), when n_tiles is at most
+                                         the persistent waves (each wave takes one tile), or for
+                                         an integrator without a probe kernel (BruteForce*,
+                                         Whitted, Mandelbrot).  For a caller's tile list each
+                                         tile's own probe time is its estimate; for a whole frame
+                                         it is blended with its image neighbours'.                  */
     int32_t        reserved[2];       /* must be 0                                                  */
 } sp_render_params;
 

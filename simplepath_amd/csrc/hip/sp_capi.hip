@@ -21,7 +21,8 @@ hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
 size_t     render_static_lds(int integ, int variant);
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream);
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, bool smooth, int32_t* order,
+                             hipStream_t stream);
 bool       has_probe(int integ);
 hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
                         hipStream_t stream);
@@ -242,15 +243,20 @@ struct sp_scene {
     // main.cpp:122-130): the render scratch above is per scene, so calls are serialised -- on the
     // host by `mu`, and on the device by making each call's stream wait for the previous call's
     // last operation (ev_done), whichever stream that call used.  A host tile list is staged
-    // through pinned memory (h_tiles) whose previous copy is waited for before it is rewritten, so
-    // the caller's array may be reused as soon as sp_render_tiles returns.
+    // through a ring of STAGE_RING pinned buffers (h_tiles), each rewritten only once its previous
+    // copy has run, so the caller's array may be reused as soon as sp_render_tiles returns.  Each
+    // staged copy is queued behind the previous call's render (ev_done), so with one buffer a third
+    // back-to-back call waited on the host for the first render; with the ring the host waits only
+    // when STAGE_RING calls are queued ahead of the copy it needs.
+    static constexpr int STAGE_RING = 4;
     std::mutex           mu;
     hipEvent_t           ev_done  = nullptr; // recorded at the end of every render call
     bool                 done_rec = false;
-    int32_t*             h_tiles  = nullptr; // pinned staging of host tile lists
-    size_t               h_tiles_cap = 0;
-    hipEvent_t           ev_tiles = nullptr; // after the staged copy
-    bool                 tiles_rec = false;
+    int32_t*             h_tiles[STAGE_RING]     = {};  // pinned staging of host tile lists
+    size_t               h_tiles_cap[STAGE_RING] = {};
+    hipEvent_t           ev_tiles[STAGE_RING]    = {};  // after each buffer's staged copy
+    bool                 tiles_rec[STAGE_RING]   = {};
+    int                  stage_next = 0;
 
     void release()
     {
@@ -293,9 +299,13 @@ struct sp_scene {
         if (probe_counters) (void)hipFree(probe_counters);
         d_tile_time = nullptr; d_order = nullptr; order_cap = 0; probe_counters = nullptr;
         if (ev_done) (void)hipEventDestroy(ev_done);
-        if (ev_tiles) (void)hipEventDestroy(ev_tiles);
-        if (h_tiles) (void)hipHostFree(h_tiles);
-        ev_done = ev_tiles = nullptr; done_rec = tiles_rec = false; h_tiles = nullptr; h_tiles_cap = 0;
+        ev_done = nullptr; done_rec = false;
+        for (int k = 0; k < STAGE_RING; ++k) {
+            if (ev_tiles[k]) (void)hipEventDestroy(ev_tiles[k]);
+            if (h_tiles[k]) (void)hipHostFree(h_tiles[k]);
+            ev_tiles[k] = nullptr; tiles_rec[k] = false; h_tiles[k] = nullptr; h_tiles_cap[k] = 0;
+        }
+        stage_next = 0;
         mt_state = nullptr; tile_counter = nullptr; counters = nullptr; d_tiles = nullptr;
         ev0 = ev1 = ev_render = nullptr;
         mt_waves = 0; d_tiles_cap = 0;
@@ -884,7 +894,7 @@ static int scene_upload_impl(sp_scene* s, int32_t device, const sp_upload_params
     SP_HIP(hipEventCreate(&s->ev0));
     SP_HIP(hipEventCreate(&s->ev1));
     SP_HIP(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
-    SP_HIP(hipEventCreateWithFlags(&s->ev_tiles, hipEventDisableTiming));
+    for (hipEvent_t& e : s->ev_tiles) SP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return SP_OK;
 }
 
@@ -1011,19 +1021,22 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             SP_HIP(hipMalloc(&s->d_tiles, (size_t)n_tiles * sizeof(int32_t)));
             s->d_tiles_cap = (size_t)n_tiles;
         }
-        // staged through pinned memory, so the caller's array is free once this returns
-        if (s->tiles_rec) SP_HIP(hipEventSynchronize(s->ev_tiles)); // the previous staged copy is done
-        if ((size_t)n_tiles > s->h_tiles_cap) {
-            if (s->h_tiles) (void)hipHostFree(s->h_tiles);
-            s->h_tiles     = nullptr;
-            s->h_tiles_cap = 0;
-            SP_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_tiles), (size_t)n_tiles * sizeof(int32_t), hipHostMallocDefault));
-            s->h_tiles_cap = (size_t)n_tiles;
+        // staged through the next pinned buffer of the ring, so the caller's array is free once this
+        // returns; the host waits only if that buffer's copy (STAGE_RING calls back) has not run
+        const int k = s->stage_next;
+        s->stage_next = (k + 1) % sp_scene::STAGE_RING;
+        if (s->tiles_rec[k]) SP_HIP(hipEventSynchronize(s->ev_tiles[k]));
+        if ((size_t)n_tiles > s->h_tiles_cap[k]) {
+            if (s->h_tiles[k]) (void)hipHostFree(s->h_tiles[k]);
+            s->h_tiles[k]     = nullptr;
+            s->h_tiles_cap[k] = 0;
+            SP_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_tiles[k]), (size_t)n_tiles * sizeof(int32_t), hipHostMallocDefault));
+            s->h_tiles_cap[k] = (size_t)n_tiles;
         }
-        std::memcpy(s->h_tiles, p->tile_ids, (size_t)n_tiles * sizeof(int32_t));
-        SP_HIP(hipMemcpyAsync(s->d_tiles, s->h_tiles, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream));
-        SP_HIP(hipEventRecord(s->ev_tiles, stream));
-        s->tiles_rec = true;
+        std::memcpy(s->h_tiles[k], p->tile_ids, (size_t)n_tiles * sizeof(int32_t));
+        SP_HIP(hipMemcpyAsync(s->d_tiles, s->h_tiles[k], (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+        SP_HIP(hipEventRecord(s->ev_tiles[k], stream));
+        s->tiles_rec[k] = true;
         d_ids = s->d_tiles;
     }
     if (s->n_cu == 0) {
@@ -1347,7 +1360,9 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
             SP_HIP(spd::launch_probe(sc_run, pr, integ, variant, blocks, lds_bytes, stream));
-            SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, s->d_order, stream));
+            // cost estimates blended with queue neighbours only for a whole frame, where those are
+            // the tiles left and right (a caller's list may put unrelated tiles side by side)
+            SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, !listed, s->d_order, stream));
             SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
             a.order = s->d_order;
             launches += 2;

@@ -147,6 +147,15 @@ constexpr int RSQ_HDR = 8;
 #ifndef SP_MT_BLK
 #define SP_MT_BLK 4
 #endif
+// Everything that depends on the block size -- this layout, and all of sp_path.hpp / the megakernel
+// body built on it -- lives in an inline namespace named after it (spd::mt_blk4, spd::mt_blk1), so
+// the sample-chunk TU (MT_BLK 1) and the others (4) never define one inline function two ways (the
+// one-definition rule holds even with -fgpu-rdc or a host caller).  The host-visible launch
+// interfaces (sp_mega.hpp, sp_chunk.hpp, sp_wave.hpp) and the shared records stay in spd.
+#define SPD_CAT2_(a, b) a##b
+#define SPD_CAT_(a, b) SPD_CAT2_(a, b)
+#define SPD_LAYOUT_NS SPD_CAT_(mt_blk, SP_MT_BLK)
+inline namespace SPD_LAYOUT_NS {
 constexpr int MT_BLK       = SP_MT_BLK;
 // no padding: every translation unit sizes a generation buffer the same (the sample-chunk TU keeps
 // its own block size for its generator store, sp_chunk.hip)
@@ -154,6 +163,7 @@ static_assert(spm::MT_N % MT_BLK == 0, "MT_BLK must divide 312");
 constexpr int MT_ROWS      = (spm::MT_N + MT_BLK - 1) / MT_BLK;
 constexpr int MT_GEN_WORDS = MT_ROWS * MT_BLK * 64; // words of one generation buffer of a wave slot
 __host__ __device__ inline size_t mt_off(int k) { return (size_t)(k / MT_BLK) * (64 * MT_BLK) + (size_t)(k % MT_BLK); }
+} // inline namespace SPD_LAYOUT_NS
 __host__ __device__ inline int rsqrt_words(const Scene& sc) { return RSQ_HDR + (sc.rsqrt_shift ? (1 << sc.rsqrt_bits) : (2 << sc.rsqrt_bits)); }
 
 

@@ -70,16 +70,17 @@ __device__ __forceinline__ int tile_class(float t, float thr)
 #define SP_TILE_SMOOTH 1
 #endif
 // a tile's cost estimate: its probe time blended with its queue neighbours' (for a whole frame: the
-// tiles left and right of it), against the one-sample probe's noise (profiles/r04/tile_classes/
+// tiles left and right of it; smooth = false for a caller's tile list, whose queue neighbours need
+// not be image neighbours), against the one-sample probe's noise (profiles/r04/tile_classes/
 // ab_smooth.txt: bunny +0.3-0.5 %, lucy +0.6 %, elf's 8-way shard level; SP_TILE_SMOOTH 0: the probe
 // time alone)
-__device__ __forceinline__ float tile_est(const float* t, int64_t i, int64_t n)
+__device__ __forceinline__ float tile_est(const float* t, int64_t i, int64_t n, bool smooth)
 {
-    if (!SP_TILE_SMOOTH) return t[i];
+    if (!SP_TILE_SMOOTH || !smooth) return t[i];
     const float l = t[i > 0 ? i - 1 : i], r = t[i + 1 < n ? i + 1 : i];
     return 0.25f * (l + r) + 0.5f * t[i];
 }
-__global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time, int64_t n, float factor, int32_t* order)
+__global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time, int64_t n, float factor, bool smooth, int32_t* order)
 {
     __shared__ float s_sum[16];
     __shared__ int   s_cnt[TILE_CLASSES][16];
@@ -96,7 +97,7 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time
     // class sizes -> each class's first position (classes in order 0, 1, ...)
     for (int k = 0; k < TILE_CLASSES; ++k) {
         int cnt = 0;
-        for (int64_t i = tid; i < n; i += 1024) cnt += tile_class(tile_est(tile_time, i, n), thr) == k ? 1 : 0;
+        for (int64_t i = tid; i < n; i += 1024) cnt += tile_class(tile_est(tile_time, i, n, smooth), thr) == k ? 1 : 0;
         for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
         if (lane == 0) s_cnt[k][wave] = cnt;
     }
@@ -112,7 +113,7 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time
     for (int64_t c0 = 0; c0 < n; c0 += 1024) {
         const int64_t i   = c0 + tid;
         const bool    v   = i < n;
-        const int     cls = v ? tile_class(tile_est(tile_time, i, n), thr) : -1;
+        const int     cls = v ? tile_class(tile_est(tile_time, i, n, smooth), thr) : -1;
         uint32_t      pos = 0;
         for (int k = 0; k < TILE_CLASSES; ++k) {
             const uint64_t  m = __ballot(cls == k);
@@ -134,9 +135,10 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time
     }
 }
 
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream)
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, bool smooth, int32_t* order,
+                             hipStream_t stream)
 {
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_time, n_tiles, factor, order);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_time, n_tiles, factor, smooth, order);
     return hipGetLastError();
 }
 

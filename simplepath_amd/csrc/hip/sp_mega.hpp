@@ -6,6 +6,7 @@
 #include "sp_path.hpp"
 
 namespace spd {
+inline namespace SPD_LAYOUT_NS {
 
 constexpr int WAVES_PER_BLOCK = 4;
 
@@ -148,6 +149,7 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_probe_kernel(Sc
 {
     render_tiles_body<INTEG, true>(sc, args);
 }
+} // inline namespace SPD_LAYOUT_NS
 
 using KernelFn = void (*)(Scene, RenderArgs);
 KernelFn mega_direct(int variant);
@@ -157,6 +159,7 @@ KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 KernelFn probe_direct(int variant); // nullptr: no probe kernel (queue order)
 KernelFn probe_rrnee(int waves);
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int32_t* order, hipStream_t stream);
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, bool smooth, int32_t* order,
+                             hipStream_t stream);
 
 } // namespace spd

@@ -16,6 +16,7 @@
 #include "sp_device.hpp"
 
 namespace spd {
+inline namespace SPD_LAYOUT_NS { // sp_device.hpp: one namespace per RNG state layout
 
 using namespace spm;
 
@@ -3091,4 +3092,5 @@ __device__ __forceinline__ uint32_t morton_decode_1(uint32_t a)
     return a;
 }
 
+} // inline namespace SPD_LAYOUT_NS
 } // namespace spd

@@ -9,6 +9,7 @@
 // reproduces RSQRTSS bit for bit with one table load (spm::rsqrtss_emulated).
 #include "sp_host.hpp"
 
+#include <algorithm>
 #include <atomic>
 #include <memory>
 #include <mutex>
@@ -76,9 +77,11 @@ const RsqrtCapture& rsqrt_capture()
 }
 
 namespace {
-// Installed tables are immutable and never freed (a process installs a handful at most), so a
-// reader's pointer stays valid while another thread installs the next one: no lock on the read
-// path, which runs once per normalize() of every mesh normal while a scene is built.
+// Installed tables are immutable and never freed, so a reader's pointer stays valid while another
+// thread installs the next one: no lock on the read path, which runs once per normalize() of every
+// mesh normal while a scene is built.  An install that equals a table already kept reuses it, so
+// the set grows only with the number of DISTINCT tables a process installs (a handful: one per
+// CPU whose images it reproduces), however often sp_rsqrt_table_set is called.
 std::mutex                               g_override_mu;
 std::vector<std::unique_ptr<RsqrtCapture>> g_installed; // owned for the life of the process
 std::atomic<const RsqrtCapture*>         g_override{ nullptr };
@@ -103,9 +106,16 @@ void rsqrt_set_override(const uint32_t* entries, int32_t bits, uint32_t zero_res
     if (bits < 1 || bits > k_max_table_bits)
         throw SpError(SP_ERR_ARG, "RSQRTSS table: bits must be 1.." + std::to_string(k_max_table_bits) +
                                       " (2 << bits entries must fit the device's LDS copy)");
+    const size_t n = size_t(2) << bits;
+    for (const auto& kept : g_installed)
+        if (kept->bits == bits && kept->zero_result == zero_result && kept->denorm_result == denorm_result &&
+            std::equal(entries, entries + n, kept->entries.begin())) {
+            g_override.store(kept.get(), std::memory_order_release);
+            return;
+        }
     auto cap           = std::make_unique<RsqrtCapture>();
     cap->bits          = bits;
-    cap->entries.assign(entries, entries + (size_t(2) << bits));
+    cap->entries.assign(entries, entries + n);
     cap->zero_result   = zero_result;
     cap->denorm_result = denorm_result;
     cap->verified      = true; // as given: the table of the CPU that produced the reference

@@ -13,7 +13,7 @@ _libs = {}
 
 
 def build() -> None:
-    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True, timeout=600)
 
 
 def load(variant: str = "spm"):

@@ -19,7 +19,7 @@ EXE = os.path.join(ROOT, "tests", "cpp", "_build", "drop_in_main")
 @pytest.fixture(scope="module")
 def exe():
     if os.path.isdir("/root/reference") or not os.path.exists(EXE):  # build container: (re)build it
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True, timeout=600)
     return EXE
 
 

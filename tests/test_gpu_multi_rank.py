@@ -5,32 +5,24 @@ path, and the frame assembled on rank 0 must equal one process rendering every t
 bit.  Shards this small run on the sample-chunk pipeline (AUTO below 24000 tiles), the full
 frame here on the wavefront, so this also checks that the two agree through the multi-rank path."""
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
+
+from tests._ranks import file_init_method, spawn_ranks
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _worker(rank, world, port, scene_path, w, h, spp, result_path):
+def _worker(rank, world, init_method, scene_path, w, h, spp, result_path):
     import datetime
     import sys
 
     sys.path.insert(0, ROOT)
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    dist.init_process_group("gloo", init_method=init_method, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     import simplepath_amd as sp
     from simplepath_amd import shard
 
@@ -57,8 +49,7 @@ def test_two_ranks_on_device_match_single_process(scene_dir, tmp_path):
     w, h, spp, world = 200, 120, 2, 2  # 375 tiles: ragged shards (188 + 187)
     path = os.path.join(scene_dir, "bunny.sp")
     out = str(tmp_path / "frame.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), path, w, h, spp, out), nprocs=world, join=True,
-                       start_method="spawn")
+    spawn_ranks(_worker, (world, file_init_method(tmp_path), path, w, h, spp, out), world, 270)
     frame = np.load(out)
     scene = sp.Scene.from_file(path)
     scene.set_resolution(w, h)
@@ -69,16 +60,14 @@ def test_two_ranks_on_device_match_single_process(scene_dir, tmp_path):
     assert np.array_equal(frame.view(np.uint32), ref.view(np.uint32))
 
 
-def _nccl_worker(rank, world, port, result_path):
+def _nccl_worker(rank, world, init_method, result_path):
     """Renders its shard on device `rank`, gathers the CUDA tile buffers over RCCL."""
     import datetime
     import sys
 
     sys.path.insert(0, ROOT)
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(rank)
-    dist.init_process_group("nccl", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120),
+    dist.init_process_group("nccl", init_method=init_method, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120),
                             device_id=torch.device(f"cuda:{rank}"))
     from simplepath_amd import shard
 
@@ -103,7 +92,7 @@ def test_rccl_gather_frame_on_device(tmp_path, world):
     if torch.cuda.device_count() < world:
         pytest.skip(f"needs {world} GPUs")
     out = str(tmp_path / "frame.npy")
-    mp.start_processes(_nccl_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    spawn_ranks(_nccl_worker, (world, file_init_method(tmp_path), out), world, 150)
     frame = np.load(out)
     assert frame.shape == (45, 64, 3)
     assert np.array_equal(frame, np.broadcast_to(np.arange(45, dtype=np.float32)[:, None, None], frame.shape))

@@ -16,13 +16,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def checker(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("libm") / "libm_ex")
     subprocess.run(["g++", "-O2", "-std=c++17", "-mavx2", "-mfma", "-ffp-contract=off", "-fno-builtin", "-pthread",
-                    os.path.join(ROOT, "tools", "libm_exhaustive.cpp"), "-o", exe, "-lm"], check=True)
+                    os.path.join(ROOT, "tools", "libm_exhaustive.cpp"), "-o", exe, "-lm"], check=True, timeout=300)
     return exe
 
 
 @pytest.mark.parametrize("fn", ["expf", "logf", "sinf", "cosf", "erff", "acosf", "atanf", "fmod1", "roundf", "powf", "atan2f"])
 def test_libm_matches_glibc(checker, fn):
-    out = subprocess.run([checker, fn, "4099", "4"], capture_output=True, text=True)
+    out = subprocess.run([checker, fn, "4099", "4"], capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stdout
     assert "mismatches=0" in out.stdout
 

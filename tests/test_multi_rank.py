@@ -3,30 +3,22 @@
 is the same code bench.py runs over RCCL), the frame-end gather brings them to rank 0, and the
 assembled frame must equal a single-process render of all tiles."""
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
+
+from tests._ranks import file_init_method, spawn_ranks
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _worker(rank, world, port, scene_path, w, h, spp, result_path):
+def _worker(rank, world, init_method, scene_path, w, h, spp, result_path):
     import sys
     sys.path.insert(0, ROOT)
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     import datetime
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    dist.init_process_group("gloo", init_method=init_method, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     import simplepath_amd as sp
     from simplepath_amd import shard
     from tests import _oracle
@@ -56,8 +48,7 @@ def test_gather_frame_matches_single_process(scene_dir, tmp_path, world):
     w, h, spp = 40, 24, 2  # 15 tiles: ragged shards for world 2 (8 + 7) and world 3
     path = os.path.join(scene_dir, "bunny.sp")
     out = str(tmp_path / "frame.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), path, w, h, spp, out), nprocs=world,
-                       join=True, start_method="spawn")
+    spawn_ranks(_worker, (world, file_init_method(tmp_path), path, w, h, spp, out), world, 270)
     frame = np.load(out)
     scene = sp.Scene.from_file(path)
     scene.set_resolution(w, h)

@@ -104,7 +104,11 @@ def test_rsqrt_table_override_concurrent_readers(scene_dir):
     stop = threading.Event()
 
     def writer():
-        while not stop.is_set():
+        # bounded: a slow box must not turn this into an install storm (each install used to be
+        # kept forever; now equal tables are reused, see test_rsqrt_table_set_is_bounded)
+        for _ in range(20000):
+            if stop.is_set():
+                break
             sp.set_rsqrt_table(t)
             sp.set_rsqrt_table(None)
 
@@ -124,6 +128,34 @@ def test_rsqrt_table_override_concurrent_readers(scene_dir):
         sp.set_rsqrt_table(None)
 
 
+def _rss_bytes():
+    with open("/proc/self/statm") as f:
+        return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+
+
+def test_rsqrt_table_set_is_bounded():
+    # sp_rsqrt_table_set keeps every DISTINCT installed table alive (readers hold raw pointers), but
+    # re-installing an equal table reuses the kept copy: 10 000 installs of two tables must not grow
+    # the process (each copy is 8-32 KB, so a leak would be 80-320 MB)
+    import simplepath_amd as sp
+
+    t = sp.rsqrt_table()
+    other = dict(t, entries=t["entries"] + np.uint32(1))
+    try:
+        for _ in range(200):  # warm-up: both tables installed once, allocator settled
+            sp.set_rsqrt_table(t)
+            sp.set_rsqrt_table(other)
+        before = _rss_bytes()
+        for i in range(10000):
+            sp.set_rsqrt_table(t if i & 1 else other)
+        grown = _rss_bytes() - before
+        assert grown < 50 * 2**20, grown
+        assert np.array_equal(sp.rsqrt_table()["entries"], t["entries"])  # the last one installed
+    finally:
+        sp.set_rsqrt_table(None)
+    assert np.array_equal(sp.rsqrt_table()["entries"], t["entries"])
+
+
 def test_grouped_twist_matches_libstdcxx(tmp_path):
     # the device's 4-word grouped twist (sp_twist4.h, used with the lane-blocked state layout)
     # compiled for the host: 5 consecutive generations x 3 seeds x 4 lane positions, every word
@@ -132,7 +164,8 @@ def test_grouped_twist_matches_libstdcxx(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = str(tmp_path / "twist4_check")
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "simplepath_amd", "csrc", "common"),
-                    os.path.join(root, "tests", "cpp", "twist4_check.cpp"), "-o", exe], check=True)
-    r = subprocess.run([exe], capture_output=True, text=True)
+                    os.path.join(root, "tests", "cpp", "twist4_check.cpp"), "-o", exe], check=True,
+                   timeout=300)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatching" in r.stdout

@@ -28,7 +28,7 @@ def ref():
     if not os.path.exists(REF_LIB):
         if os.path.isdir("/root/reference"):
             import subprocess
-            subprocess.run(["bash", os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
+            subprocess.run(["bash", os.path.join(ROOT, "oracle", "build_ref.sh")], check=True, timeout=1200)
         else:
             pytest.skip("reference sources not present: oracle/_ref not built")
     L = C.CDLL(REF_LIB)

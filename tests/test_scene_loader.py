@@ -289,10 +289,11 @@ def test_render_calls_from_many_threads_fail_cleanly(scene_dir):
                 codes.append(e.code)
                 msgs.append(str(e))
 
-    th = [threading.Thread(target=work) for _ in range(8)]
+    th = [threading.Thread(target=work, daemon=True) for _ in range(8)]
     for t in th:
         t.start()
     for t in th:
-        t.join()
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a render call never returned (scene lock held?)"
     assert len(codes) == 1600 and set(codes) == {_abi.SP_ERR_STATE}
     assert all("sp_scene_upload must be called" in m or "before rendering" in m for m in msgs)

@@ -8,6 +8,7 @@ patterns: wf_init's 8-byte-per-lane MT seeding stores (known 2512 B per pixel) a
 
 Usage: python3 tools/pmc_traffic.py <pmc dir with p1 (FETCH) and p2 (WRITE)> <width> <height> <spp> <out.json>
 """
+import re
 import collections
 import csv
 import glob
@@ -22,7 +23,7 @@ def kernel_key(name):
     k = name.replace("(anonymous namespace)::", "")
     if k.startswith("void "):
         k = k[5:]
-    return k.split("(")[0].split("<")[0].replace("spd::", "")
+    return k.split("(")[0].split("<")[0].split("::")[-1]
 
 
 def per_kernel(root, counter):
@@ -49,7 +50,7 @@ def main():
         n = max(len(f), len(wr), 1)
         fb = 2.0 * 1024.0 * sum(f) / max(len(f), 1)
         wb = 1024.0 * sum(wr) / max(len(wr), 1)
-        kernels[k.replace("spd::", "")] = {"dispatches": n, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+        kernels[re.sub(r"\bspd::(mt_blk\d+::)?", "", k)] = {"dispatches": n, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                                            "hbm_bytes_per_launch": fb + wb}
     dom = "wf_shade" if "wf_shade" in kernels else max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
     res = {"width": w, "height": h, "spp": spp, "scene": scene, "sim_world": sim_world, "kernel": dom,

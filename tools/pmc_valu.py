@@ -38,7 +38,7 @@ def kernel_key(name):
     k = name.replace("(anonymous namespace)::", "")
     if k.startswith("void "):
         k = k[5:]
-    return k.split("(")[0].split("<")[0].replace("spd::", "")
+    return k.split("(")[0].split("<")[0].split("::")[-1]
 
 
 def load(root):
