@@ -404,6 +404,19 @@ def stage_bytes(st, pixels):
     }
 
 
+def pmc_of_this_build(doc):
+    """A committed PMC pass counts for this line only if it profiled the library this process
+    loaded: its sp_build_id (tools/pmc_traffic.py / pmc_valu.py read it from the profiled bench
+    runs) must equal the loaded build's.  Passes of another build -- or of none recorded -- give
+    null traffic / valu, so a line never quotes counters of code it did not run."""
+    try:
+        import simplepath_amd as sp
+        mine = sp._abi.build_identity()["build_id"]
+    except Exception:
+        return False
+    return doc.get("sp_build_id") is not None and doc.get("sp_build_id") == mine
+
+
 def valu_of(args, kernel):
     """VALU-issue roofline of `kernel` from a committed PMC pass of the same workload
     (tools/gpu_pmc_valu.sh -> tools/pmc_valu.py): issue cycles of its VALU instructions (f32/int
@@ -417,13 +430,19 @@ def valu_of(args, kernel):
     if (vj.get("width"), vj.get("height"), vj.get("spp"), vj.get("scene", "bunny"), vj.get("sim_world", 0)) != \
             (args.width, args.height, args.spp, args.scene, args.sim_world):
         return None
+    if not pmc_of_this_build(vj):
+        return None
     k = vj.get("kernels", {}).get(kernel)
     if not k:
         return None
     return {"frac": round(k["valu_frac"], 4), "wait_frac": round(k.get("wait_frac", 0.0), 4),
-            "lane_util": round(k.get("lane_util", 0.0), 4), "kernel": kernel,
+            "lane_util": round(k.get("lane_util", 0.0), 4), "kernel": kernel, "sp_build_id": vj["sp_build_id"],
             "valu_insts_per_launch": k["valu_insts"], "kernel_ms_profiled": round(k["ms_profiled"], 4),
             "source": os.path.relpath(args.valu_json, ROOT)}
+
+
+def traffic_source(args, tj):
+    return None if tj is None else {"file": os.path.relpath(args.traffic_json, ROOT), "sp_build_id": tj.get("sp_build_id")}
 
 
 def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
@@ -440,7 +459,8 @@ def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
             if (tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp
-                    and tj.get("scene", "bunny") == args.scene and tj.get("sim_world", 0) == args.sim_world):
+                    and tj.get("scene", "bunny") == args.scene and tj.get("sim_world", 0) == args.sim_world
+                    and pmc_of_this_build(tj)):
                 traffic = tj.get("hbm_bytes_per_launch")
             else:
                 tj = None
@@ -456,6 +476,7 @@ def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
             traffic = sum(v["hbm_bytes_per_launch"] for k, v in tj.get("kernels", {}).items() if k.startswith("ck_")) or traffic
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "ck_camera+ck_count+ck_shade+ck_sum",
+                "traffic_source": traffic_source(args, tj),
                 "scene_bytes": scene_bytes,
                 "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg,
                 "valu": valu_of(args, "ck_shade")}  # the shading kernel: most of the four kernels' time
@@ -472,6 +493,7 @@ def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
             traffic = tj["kernels"]["sp_render_kernel"]["hbm_bytes_per_launch"]
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "sp_render_kernel",
+                "traffic_source": traffic_source(args, tj),
                 "scene_bytes": scene_bytes,
                 "kernel_ms": round(render_ms, 3), "probe_ms": round(probe_ms, 3), "alg_bytes_per_launch": alg,
                 "valu": valu_of(args, "sp_render_kernel")}

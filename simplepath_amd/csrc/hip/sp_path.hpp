@@ -555,6 +555,8 @@ struct Isect {
     float t;
     f3    n, p;
     int   material;
+    bool  unbounded; // on an unbounded shape (plane): outside the BVH, so the shadow ray's walk has
+                     // no leaves of its own origin (wide_any_packet)
 };
 
 // Shape-specific surface data for the final closest hit (identical arithmetic to the reference,
@@ -566,6 +568,7 @@ __device__ __forceinline__ Isect finish_hit(const Scene& sc, const Hit& h, const
     const uint32_t id   = h.code & CODE_MASK;
     is.t = h.t;
     is.p = ray_at(ray, h.t);
+    is.unbounded = kind == KIND_PLANE;
     if (kind == KIND_TRI) {
         const uint32_t i0 = sc.indices[3 * id], i1 = sc.indices[3 * id + 1], i2 = sc.indices[3 * id + 2];
         const f3 n0 = mk(sc.normals[3 * i0], sc.normals[3 * i0 + 1], sc.normals[3 * i0 + 2]);
@@ -876,6 +879,145 @@ __device__ __forceinline__ uint32_t key_mask(uint32_t m, uint32_t o)
     m = (o & 2u) ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
     m = (o & 4u) ? (((m & 0x0fu) << 4) | ((m >> 4) & 0x0fu)) : m;
     return m;
+}
+
+// ---------------------------------------------------------------- any-hit walk as one wave packet
+// DirectLighting's shadow rays of one 8x8 tile all end on the same light, so their walks over the
+// 8-wide BVH visit nearly the same nodes -- but each lane fetched them itself: five dwordx4 loads
+// per node, each a vector-L1 tag lookup per active lane (61 lookups per VMEM instruction in the
+// bunny frame, round 4), at 0.29 walk-step lane occupancy.  Here the wave walks ONE node sequence,
+// the union of its lanes' walks: the node index is wave-uniform, so the node (80 B) and the leaf
+// triangles (48 B each) are fetched once for the wave with scalar loads, and every lane box-tests
+// and triangle-tests its own ray.  A lane takes part in a node only if its own walk would visit
+// it -- its ray hit that node's box in the parent, and the parent's box before that (per-lane
+// child masks on the LDS stack) -- so each lane tests exactly the primitives its per-lane walk
+// (wide_any) would, and its answer, an OR over that set, is the same bit.  Lanes that found a hit
+// drop out; the walk ends when every lane has one or the union is exhausted.  Traversal order
+// follows the octant of the wave's first lane.  Incoherent packets (a tile straddling a
+// silhouette) make the union long: after SP_PACKET_BUDGET node steps the lanes still unresolved
+// finish with their own per-lane walks from the root (re-testing primitives does not change an OR).
+// Stack: per level, each lane's own inner-child mask (slot order) in row sp, and the wave's
+// pending group {child_base << 8 | union key mask} in row sp + depth / 2 (written alike by every
+// lane, read back with readfirstlane); needs the wide closest-hit stack layout (Scene::wide_closest).
+// SP_RENDER_PER_LANE_QUERIES (Scene::merge_queries = 0) keeps the per-lane walks, for comparison.
+#ifndef SP_PACKET_ANY
+#define SP_PACKET_ANY 0
+#endif
+#ifndef SP_PACKET_BUDGET
+#define SP_PACKET_BUDGET 0 // node steps before the per-lane fallback; 0 = none
+#endif
+typedef const __attribute__((address_space(4))) uint32_t cu32; // scalar (constant) loads, below too
+__device__ __forceinline__ uint4 uload4(cu32* q, int i) { return make_uint4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]); }
+__device__ __forceinline__ uint32_t ufirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+template <class T>
+__device__ __forceinline__ const T* uniform_ptr(const T* p)
+{
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    return (const T*)(uintptr_t)(((uint64_t)ufirst((uint32_t)(a >> 32)) << 32) | ufirst((uint32_t)a));
+}
+__device__ __forceinline__ bool wide_any_packet(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+{
+    const f3       inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    const uint32_t ou   = ufirst(dir_sign_bits(ray.d)); // the packet's visiting order
+    const int      half = st.depth >> 1;
+    uint32_t*      own  = st.s + st.lane;               // row e: own[e * 64]
+    uint32_t*      uni  = st.s + half * 64 + st.lane;   // row e: uni[e * 64]
+    int            sp   = 0;
+    uint32_t       node = 0;
+    bool           mine = true, hit = false;
+    int            steps = 0;
+    while (true) {
+#ifdef SP_WAVE_PROF
+        const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 7: any-hit walk steps
+#endif
+        cu32* np = (cu32*)uniform_ptr(sc.wnodes + 5 * (size_t)node);
+        const uint4 w0 = uload4(np, 0), w1 = uload4(np, 1), w2 = uload4(np, 2), w3 = uload4(np, 3), w4 = uload4(np, 4);
+        const float px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
+        const float sx = __uint_as_float((w0.w & 0xffu) << 23);
+        const float sy = __uint_as_float(((w0.w >> 8) & 0xffu) << 23);
+        const float sz = __uint_as_float(((w0.w >> 16) & 0xffu) << 23);
+        const uint32_t imask = w0.w >> 24;
+        const bool     live  = mine && !hit;
+        uint32_t       my_inner = 0, my_leaf = 0, u_inner = 0, u_leaf = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t meta  = ((k < 4 ? w1.z : w1.w) >> (8 * (k & 3))) & 0xffu;
+            const bool     inner = (imask >> k) & 1u;
+            if (!inner && meta == 0u) continue;
+            const int   h  = k >> 2;
+            const float lx = fma_f(ubyte(h ? w2.y : w2.x, k), sx, px);
+            const float ly = fma_f(ubyte(h ? w2.w : w2.z, k), sy, py);
+            const float lz = fma_f(ubyte(h ? w3.y : w3.x, k), sz, pz);
+            const float hx = fma_f(ubyte(h ? w3.w : w3.z, k), sx, px);
+            const float hy = fma_f(ubyte(h ? w4.y : w4.x, k), sy, py);
+            const float hz = fma_f(ubyte(h ? w4.w : w4.z, k), sz, pz);
+            float       t0;
+            const bool  b   = live && wbox(lx, ly, lz, hx, hy, hz, ray, inv, tmin, tmax, t0);
+            const bool  any = __ballot(b) != 0;
+            if (inner) { my_inner |= (b ? 1u : 0u) << k; u_inner |= (any ? 1u : 0u) << k; }
+            else { my_leaf |= (b ? 1u : 0u) << k; u_leaf |= (any ? 1u : 0u) << k; }
+        }
+        for (uint32_t m = u_leaf; m; m &= m - 1) {
+            const int      k    = __ffs(m) - 1;
+            const uint32_t meta = ((k < 4 ? w1.z : w1.w) >> (8 * (k & 3))) & 0xffu;
+            const uint32_t base = w1.y + (meta & 31u);
+            const bool     test = (my_leaf >> k) & 1u;
+            for (uint32_t j = 0; j < (meta >> 5); ++j) {
+                cu32* tp = (cu32*)uniform_ptr(sc.wslot_tri + 3 * (size_t)(base + j));
+                const uint4    a0 = uload4(tp, 0), a1 = uload4(tp, 1), a2 = uload4(tp, 2);
+                const uint32_t code = a0.w;
+                if ((code >> CODE_SHIFT) == KIND_TRI) {
+                    const float4 q0 = make_float4(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z), 0.0f);
+                    const float4 q1 = make_float4(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z), 0.0f);
+                    const float4 q2 = make_float4(__uint_as_float(a2.x), __uint_as_float(a2.y), __uint_as_float(a2.z), 0.0f);
+                    float t, be, ga;
+                    if (test && !hit && tri_hit(q0, q1, q2, ray, tmin, tmax, t, be, ga)) hit = true;
+                } else if (test && !hit) {
+                    hit = prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri);
+                }
+            }
+        }
+#ifdef SP_WAVE_PROF
+        wprof_end(7, t_it);
+#endif
+        if (__ballot(!hit) == 0) return true; // every lane of the packet is occluded
+        ++steps;
+        if (SP_PACKET_BUDGET > 0 && steps >= SP_PACKET_BUDGET) break;
+        if (u_inner) {
+            const uint32_t keys = key_mask(u_inner, ou);
+            const int      kf   = __ffs(keys) - 1;
+            const uint32_t rest = keys & (keys - 1);
+            if (rest) {
+                own[sp * 64] = my_inner;
+                uni[sp * 64] = (w1.x << 8) | rest;
+                ++sp;
+            }
+            const uint32_t slot = (uint32_t)kf ^ ou;
+            node = w1.x + slot;
+            mine = (my_inner >> slot) & 1u;
+            continue;
+        }
+        bool found = false;
+        while (sp > 0) { // next pending child some unresolved lane hit
+            const uint32_t e = ufirst(uni[(sp - 1) * 64]);
+            uint32_t       m = e & 0xffu;
+            const int      k = __ffs(m) - 1;
+            m &= m - 1;
+            const uint32_t slot = (uint32_t)k ^ ou;
+            const bool     me   = (own[(sp - 1) * 64] >> slot) & 1u;
+            if (m) uni[(sp - 1) * 64] = (e & ~0xffu) | m;
+            else --sp;
+            if (__ballot(me && !hit) == 0) continue; // nobody left who needs this subtree
+            node  = (e >> 8) + slot;
+            mine  = me;
+            found = true;
+            break;
+        }
+        if (!found) return hit;
+    }
+    // budget spent: the unresolved lanes walk on their own
+    if (!hit) hit = wide_any(sc, ray, tmin, tmax, st);
+    return hit;
 }
 
 // Closest hit over the 8-wide BVH: at each node the hit leaves' primitives are tested, the
@@ -1287,11 +1429,15 @@ __device__ __forceinline__ bool unbounded_any(const Scene& sc, const Ray& ray, f
     }
     return false;
 }
+template <bool PACKET = false>
 __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     if (unbounded_any(sc, ray, tmin, tmax)) return true;
     if (sc.n_nodes == 0) return false;
-    if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
+    if (sc.wnodes) {
+        if (PACKET && sc.wide_closest && sc.merge_queries) return wide_any_packet(sc, ray, tmin, tmax, st);
+        return wide_any(sc, ray, tmin, tmax, st);
+    }
     return sc.stackless ? bvh_any<true>(sc, ray, tmin, tmax, st) : bvh_any<false>(sc, ray, tmin, tmax, st);
 }
 
@@ -1561,9 +1707,10 @@ __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, floa
 }
 
 // Scene::intersect_p (base/Scene.h:79)
+template <bool PACKET = false>
 __device__ __forceinline__ bool scene_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
-    return geometry_any(sc, ray, tmin, tmax, st) || lights_any(sc, ray, tmin, tmax, st);
+    return geometry_any<PACKET>(sc, ray, tmin, tmax, st) || lights_any(sc, ray, tmin, tmax, st);
 }
 
 // ------------------------------------------------------------------------------ sampling
@@ -2350,12 +2497,13 @@ struct Ctx {
 #define SP_PROF(k, stmt) stmt
 #endif
 
+template <bool PACKET = false>
 __device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float tmax)
 {
     ++c.shadow;
     ++c.rays;
     bool hit;
-    SP_WPROF(3, hit = scene_any(c.sc, r, tmin, tmax, c.st));
+    SP_WPROF(3, hit = scene_any<PACKET>(c.sc, r, tmin, tmax, c.st));
     return hit;
 }
 
@@ -2394,7 +2542,17 @@ __device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
         rgb      f;
         SP_PROF(2, f = material_eval(c.sc, is.material, wo, wi, is.n, c.rng, c.q));
         bool vis = false;
-        if (!cblack(f)) SP_PROF(3, vis = !occluded(c, ls.ray, ls.tmin, ls.tmax));
+        if (!cblack(f)) {
+#if SP_PACKET_ANY == 2
+            // packet walks only when every lane's shadow ray leaves an unbounded shape (a floor
+            // plane): rays leaving BVH geometry each start inside their own leaves, and the union
+            // of those neighbourhoods makes the packet's node sequence long
+            if (__ballot(!is.unbounded) == 0) SP_PROF(3, vis = !occluded<true>(c, ls.ray, ls.tmin, ls.tmax));
+            else SP_PROF(3, vis = !occluded<false>(c, ls.ray, ls.tmin, ls.tmax));
+#else
+            SP_PROF(3, vis = !occluded<SP_PACKET_ANY != 0>(c, ls.ray, ls.tmin, ls.tmax));
+#endif
+        }
         if (vis) L = cadd(L, cdivs(cscale(cmul(f, ls.L), abs_f(dot(wi, is.n))), ls.pdf));
     }
     return L;

@@ -36,6 +36,20 @@ def per_kernel(root, counter):
     return vals
 
 
+def build_id_of_passes(root):
+    """sp_build_id of the library the profiled bench runs loaded (their JSON lines, p*.json beside
+    the counter directories); None unless every pass ran the same build."""
+    ids = set()
+    for f in sorted(glob.glob(os.path.join(root, "p*.json"))):
+        try:
+            with open(f) as fh:
+                line = [x for x in fh.read().splitlines() if x.startswith("{")][-1]
+            ids.add((json.loads(line).get("library") or {}).get("build_id"))
+        except (OSError, ValueError, IndexError):
+            ids.add(None)
+    return ids.pop() if len(ids) == 1 else None
+
+
 def main():
     root, w, h, spp, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
     scene = sys.argv[6] if len(sys.argv) > 6 else "bunny"  # bench.py --scene of the profiled run
@@ -53,7 +67,7 @@ def main():
         kernels[re.sub(r"\bspd::(mt_blk\d+::)?", "", k)] = {"dispatches": n, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                                            "hbm_bytes_per_launch": fb + wb}
     dom = "wf_shade" if "wf_shade" in kernels else max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
-    res = {"width": w, "height": h, "spp": spp, "scene": scene, "sim_world": sim_world, "kernel": dom,
+    res = {"sp_build_id": build_id_of_passes(root), "width": w, "height": h, "spp": spp, "scene": scene, "sim_world": sim_world, "kernel": dom,
            "hbm_bytes_per_launch": kernels[dom]["hbm_bytes_per_launch"], "kernels": kernels,
            "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1, KiB -> bytes"}
     with open(out, "w") as fh:

@@ -62,6 +62,20 @@ def mean(x):
     return sum(x) / len(x) if x else 0.0
 
 
+def build_id_of_passes(root):
+    """sp_build_id of the library the profiled bench runs loaded (their JSON lines, p*.json beside
+    the counter directories); None unless every pass ran the same build."""
+    ids = set()
+    for f in sorted(glob.glob(os.path.join(root, "p*.json"))):
+        try:
+            with open(f) as fh:
+                line = [x for x in fh.read().splitlines() if x.startswith("{")][-1]
+            ids.add((json.loads(line).get("library") or {}).get("build_id"))
+        except (OSError, ValueError, IndexError):
+            ids.add(None)
+    return ids.pop() if len(ids) == 1 else None
+
+
 def main():
     root, w, h, spp, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
     scene = sys.argv[6] if len(sys.argv) > 6 else "bunny"  # bench.py --scene of the profiled run
@@ -95,7 +109,7 @@ def main():
             if n in m:
                 d[n] = m[n]
         res[k] = d
-    doc = {"width": w, "height": h, "spp": spp, "scene": scene, "sim_world": sim_world, "model": __doc__.split("Usage:")[0].strip(), "kernels": res}
+    doc = {"sp_build_id": build_id_of_passes(root), "width": w, "height": h, "spp": spp, "scene": scene, "sim_world": sim_world, "model": __doc__.split("Usage:")[0].strip(), "kernels": res}
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
     for k, d in sorted(res.items(), key=lambda x: -x[1]["valu_cycles"] * x[1]["dispatches"]):
