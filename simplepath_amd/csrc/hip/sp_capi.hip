@@ -1257,9 +1257,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         a.out         = d_out;
         SP_HIP(hipMemsetAsync(s->ck_ctr, 0, 2 * sizeof(int32_t), stream));
         SP_HIP(hipEventRecord(s->ev0, stream));
-        spd::Scene sc_ck    = s->dev; // the resident scene with this render's options
-        sc_ck.merge_queries = (p->flags & SP_RENDER_PER_LANE_QUERIES) ? 0 : 1; // packet shadow walks
-        SP_HIP(spd::chunk_render(sc_ck, a, blocks, s->n_cu, stream));
+        SP_HIP(spd::chunk_render(s->dev, a, blocks, s->n_cu, stream));
         launches = 4;
     } else {
         const int    rs_words  = spd::rsqrt_words(s->dev);

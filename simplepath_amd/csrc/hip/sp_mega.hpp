@@ -41,6 +41,9 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
 #ifdef SP_WAVE_PROF
     if (lane < 16) wprof_lds[wave * 16 + lane] = 0;
 #endif
+#ifdef SP_TRAFFIC_DIAG
+    if (lane < 32) tdg_lds[wave * 32 + lane] = 0;
+#endif
     __syncthreads();
     Rsq   q{ lds };
     Stack st{ lds + rs_words + wave * sc.stack_words * 64, lane, sc.stack_depth };
@@ -82,6 +85,12 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
                 c.deep    = args.deep + gwave * 64 + lane;
                 c.dstride = args.deep_stride;
             }
+#if SP_SERVE_RHO && SP_MERGE_QUERIES
+            if constexpr (INTEG == SP_INTEGRATOR_ITERATIVE_RRNEE && SP_RRNEE_REGEN) {
+                // every sample of the pixel, paths regenerated as they end (sp_path.hpp)
+                SP_WPROF(0, acc = integrate_rrnee_regen(c, px, py, seed2d, args.spp));
+            } else
+#endif
             for (uint32_t i = 0; i < args.spp; ++i) {
                 rng_prepare(rng);
                 // RSequenceSampler::get_next_2D (math/Sampler.h:158) with count i
@@ -115,7 +124,7 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
         o[0]     = acc.r;
         o[1]     = acc.g;
         o[2]     = acc.b;
-#ifndef SP_WAVE_PROF
+#if !defined(SP_WAVE_PROF) && !defined(SP_TRAFFIC_DIAG) // those builds use the buffer for their totals
         if (args.tile_diag) {
             // {t0, t1, wave, item, then per stage the largest shader-clock total of any lane}
             for (int k = 0; k < 4; ++k)
@@ -131,6 +140,9 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
     }
 #ifdef SP_WAVE_PROF
     if (args.tile_diag && lane < 16) atomicAdd(args.tile_diag + lane, wprof_lds[wave * 16 + lane]);
+#endif
+#ifdef SP_TRAFFIC_DIAG
+    if (args.tile_diag && lane < 32) atomicAdd(args.tile_diag + 16 + lane, tdg_lds[wave * 32 + lane]);
 #endif
     unsigned long long v[4] = { rays_total, shadow_total, samples_total, draws_total };
     for (int k = 0; k < 4; ++k) {

@@ -3,6 +3,8 @@
 // (sp_path.hpp SP_RHO_TOUCH): 2762 vs 2720 Mrays/s with the window of 2 (profiles/r02/s5).
 #define SP_RNG_PF 0
 #define SP_RHO_TOUCH 1
+// two consecutive draws at an even stream position: one 16-byte load (sp_path.hpp rng_raw2)
+#define SP_RNG_PAIR 1
 #include "sp_mega.hpp"
 
 namespace spd {

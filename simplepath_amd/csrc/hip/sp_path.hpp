@@ -54,6 +54,62 @@ __device__ __forceinline__ void wprof_end(int k, uint64_t t0)
 #define SP_WPROF(k, stmt) stmt
 #endif
 
+// ============================================================================ traffic by source
+// Diagnostic build only (-DSP_TRAFFIC_DIAG, tools/gpu_traffic_diag.sh): for each source of memory
+// requests, the distinct 128-byte lines each wave-level access touches (what the vector L1 asks of
+// L2 when it misses) and the bytes the lanes asked for.  Sources: 8-wide BVH nodes, wide-leaf
+// triangle records, binary BVH slot records, closest-hit records (indices, normals, material), the
+// RNG draws of a lane's own stream, the LDS-DMA touches ahead of a glossy estimate, the words
+// another lane's served estimate reads, twists (read + write of a generation) and seeding.  Per
+// wave in LDS, flushed to the render's tile_diag buffer (u64 slots 16 + 2k: lines, 17 + 2k: bytes)
+// at kernel end (sp_mega.hpp).
+#ifdef SP_TRAFFIC_DIAG
+enum { TD_NODE, TD_TRI, TD_BIN, TD_HIT, TD_DRAW, TD_TOUCH, TD_SERVED, TD_TWIST, TD_SEED, TD_BOUNCE, TD_N };
+static __shared__ unsigned long long tdg_lds[16 * 32];
+__device__ __forceinline__ void td_add(int cat, uint64_t lines, uint64_t bytes)
+{
+    const uint64_t m     = __ballot(1);
+    const int      first = __ffsll((unsigned long long)m) - 1;
+    if ((int)(threadIdx.x & 63) == first) {
+        const int w = threadIdx.x >> 6;
+        tdg_lds[w * 32 + 2 * cat] += lines;
+        tdg_lds[w * 32 + 2 * cat + 1] += bytes;
+    }
+}
+__device__ __forceinline__ uint32_t td_distinct(uint64_t v, uint64_t todo)
+{
+    uint32_t cnt = 0;
+    while (todo) {
+        const int      src = __ffsll((unsigned long long)todo) - 1;
+        const uint32_t lo  = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+        const uint32_t hi  = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+        todo &= ~__ballot(v == (((uint64_t)hi << 32) | lo));
+        ++cnt;
+    }
+    return cnt;
+}
+__device__ __forceinline__ void td_lines(int cat, const void* p, int nbytes)
+{
+    const uint64_t a = (uint64_t)(uintptr_t)p, l0 = a >> 7, l1 = (a + (uint64_t)nbytes - 1) >> 7;
+    const uint64_t m = __ballot(1);
+    uint32_t cnt = td_distinct(l0, m);
+    cnt += td_distinct(l1 != l0 ? l1 : ~0ull, __ballot(l1 != l0));
+    td_add(cat, cnt, (uint64_t)__popcll(m) * (uint64_t)nbytes);
+}
+// a twist by the active lanes: each reads and writes one 312-word generation; with 4-word lane
+// blocks a 128-byte line holds 4 lanes' blocks, 78 lines per 4-lane group and direction
+__device__ __forceinline__ void td_twist(int cat)
+{
+    const uint64_t m = __ballot(1);
+    uint64_t groups = 0;
+    for (int g = 0; g < 16; ++g) groups += ((m >> (4 * g)) & 0xfull) ? 1 : 0;
+    td_add(cat, groups * 78 * 2, (uint64_t)__popcll(m) * 312 * 8 * 2);
+}
+#define SP_TD(stmt) stmt
+#else
+#define SP_TD(stmt)
+#endif
+
 // ============================================================================ per-lane state
 // The RSQRTSS table as a kernel holds it (LDS copy, or the global original): t -> the header
 // {bits, zero_result, denorm_result, pack_shift, pack_hi} (sp_device.hpp), entries at t + RSQ_HDR.
@@ -112,6 +168,9 @@ struct Rng {
     // already there, so a buffer switch never twists.
     int       lin = 0, pre = 0;
     int       pfn = 0;        // valid words in pf (words idx .. idx + pfn - 1 of buffer cur)
+#ifdef SP_TRAFFIC_DIAG
+    int       td_cat = TD_DRAW; // served estimates read another lane's words: TD_SERVED
+#endif
     uint64_t  pf[RNG_PF > 0 ? RNG_PF : 1];
 #if SP_SERVE_RHO
     // Wave-served selection weights (serve_rho): the estimates of this lane's next eval / pdf /
@@ -253,6 +312,7 @@ __device__ __forceinline__ void rng_seed(Rng& r, uint32_t seed)
 __device__ __forceinline__ void rng_seed_twisted(Rng& r, uint32_t seed)
 {
     static_assert(MT_N - MT_M == MT_M, "two seed chains M apart cover words 0 .. N - 1");
+    SP_TD(td_twist(TD_SEED)); // writes a generation, reads back part of it (counted as a twist's)
     r.cur         = 0;
     uint64_t*  B  = mt_buf(r, mt_next(r));
     uint64_t   xk = (uint64_t)seed, xm = (uint64_t)seed;
@@ -304,6 +364,7 @@ __device__ __forceinline__ void rng_prepare(Rng& r)
     const bool urgent = !r.ready && r.idx >= MT_N - RNG_MARGIN;
     if (__any(urgent)) {
         if (!r.ready) {
+            SP_TD(td_twist(TD_TWIST));
             mt_twist_blocked<SP_TWIST_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
             r.ready = 1;
         }
@@ -316,7 +377,10 @@ template <bool NT = false>
 __device__ __forceinline__ uint64_t rng_raw(Rng& r)
 {
     if (r.idx >= MT_N) {
-        if (!NT && !r.ready) mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+        if (!NT && !r.ready) {
+            SP_TD(td_twist(TD_TWIST));
+            mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+        }
         r.cur   = mt_next(r);
         r.idx   = 0;
         r.ready = r.pre;
@@ -330,6 +394,7 @@ __device__ __forceinline__ uint64_t rng_raw(Rng& r)
         for (int k = 0; k + 1 < RNG_PF; ++k) r.pf[k] = r.pf[k + 1];
         --r.pfn;
     } else {
+        SP_TD(td_lines(r.td_cat, &b[mt_off(r.idx)], 8));
         w = b[mt_off(r.idx)];
     }
     ++r.idx;
@@ -337,6 +402,7 @@ __device__ __forceinline__ uint64_t rng_raw(Rng& r)
 #pragma unroll
     for (int k = 0; k < RNG_PF; ++k)
         if (r.pfn == k && r.idx + k < MT_N) {
+            SP_TD(td_lines(r.td_cat, &b[mt_off(r.idx + k)], 8));
             r.pf[k] = b[mt_off(r.idx + k)];
             r.pfn   = k + 1;
         }
@@ -350,7 +416,10 @@ __device__ __forceinline__ void rng_skip(Rng& r, int n)
 {
     while (n > 0) {
         if (r.idx >= MT_N) {
-            if (!r.ready) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+            if (!r.ready) {
+                SP_TD(td_twist(TD_TWIST));
+                mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+            }
             r.cur   = mt_next(r);
             r.idx   = 0;
             r.ready = r.pre;
@@ -399,11 +468,15 @@ __device__ __forceinline__ void rng_touch(const Rng& r, int n, __attribute__((ad
         }
     } else { // one touch per line: words idx .. idx + n - 1 of this generation, the rest of the next
         const int end = r.idx + n;
-        for (int row = r.idx; row < end && row < MT_N; row = (row / MT_BLK + 1) * MT_BLK)
+        for (int row = r.idx; row < end && row < MT_N; row = (row / MT_BLK + 1) * MT_BLK) {
+            SP_TD(td_lines(TD_TOUCH, cur + mt_off(row), 4));
             __builtin_amdgcn_global_load_lds((const void*)(cur + mt_off(row)), sink, 4, 0, 0);
+        }
         if (r.ready)
-            for (int row = 0; row < end - MT_N; row += MT_BLK)
+            for (int row = 0; row < end - MT_N; row += MT_BLK) {
+                SP_TD(td_lines(TD_TOUCH, next + mt_off(row), 4));
                 __builtin_amdgcn_global_load_lds((const void*)(next + mt_off(row)), sink, 4, 0, 0);
+            }
     }
 }
 
@@ -413,6 +486,7 @@ __device__ __forceinline__ void rng_touch(const Rng& r, int n, __attribute__((ad
 __device__ __forceinline__ void rng_reserve(Rng& r, int n)
 {
     if (!r.ready && r.idx + n > MT_N) {
+        SP_TD(td_twist(TD_TWIST));
         mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
         r.ready = 1;
     }
@@ -430,6 +504,48 @@ __device__ __forceinline__ void rng_reserve(Rng& r, int n)
 static __shared__ uint32_t rho_rng_sink[64];
 #endif
 
+// Two consecutive draws.  With lane blocks of 4 words (MT_BLK >= 2) words 2j and 2j + 1 of a
+// generation are one aligned 16-byte pair, so two draws that start at an even position are one
+// dwordx4 load instead of two dwordx2 loads: half the wave-level RNG loads -- and half the
+// vector-L1 tag lookups -- where lanes read scattered streams (a served estimate reads 32 words of
+// ANOTHER lane's stream: per wave instruction up to 64 lines, the largest source of lookups in the
+// elf frame).  Same words in the same order (a generation has an even number of
+// words, so a pair never straddles two); at an odd position the draws are taken one by one.
+// Per translation unit: on in the DirectLighting megakernel (bunny 1080p @ 256 spp +0.2-0.5 %,
+// spheres 1024^2 @ 64 spp +1-3 %), off in IterativeRRNEE's (elf 1024^2 @ 16 spp 1028-1031 ->
+// 993-998, its 8-way shard 1220-1224 -> 1174-1179 Mrays/s; profiles/r05/rng_pair/).
+#ifndef SP_RNG_PAIR
+#define SP_RNG_PAIR 0
+#endif
+template <bool NT = false>
+__device__ __forceinline__ void rng_raw2(Rng& r, uint64_t& w0, uint64_t& w1)
+{
+    if constexpr (SP_RNG_PAIR && MT_BLK >= 2 && RNG_PF == 0) {
+        if (r.idx >= MT_N) { // the buffer switch of rng_raw
+            if (!NT && !r.ready) {
+                SP_TD(td_twist(TD_TWIST));
+                mt_twist_into(mt_buf(r, r.cur), mt_buf(r, mt_next(r)));
+            }
+            r.cur   = mt_next(r);
+            r.idx   = 0;
+            r.ready = r.pre;
+            r.pfn   = 0;
+        }
+        if ((r.idx & 1) == 0) {
+            const uint64_t* b = mt_buf(r, r.cur) + mt_off(r.idx);
+            SP_TD(td_lines(r.td_cat, b, 16));
+            const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(b);
+            w0 = mt_temper(p.x);
+            w1 = mt_temper(p.y);
+            r.idx += 2;
+            r.draws += 2;
+            return;
+        }
+    }
+    w0 = rng_raw<NT>(r);
+    w1 = rng_raw<NT>(r);
+}
+
 // IncoherentSampler::get_next_1D / get_next_2D (math/Sampler.h:110-118)
 template <bool NT = false>
 __device__ __forceinline__ float next1D(Rng& r) { return canonical_from_u64(rng_raw<NT>(r)); }
@@ -438,9 +554,11 @@ struct P2 {
 };
 __device__ __forceinline__ P2 next2D(Rng& r)
 {
+    uint64_t a, b;
+    rng_raw2(r, a, b);
     P2 p;
-    p.x = next1D(r); // braced-init-list: left-to-right
-    p.y = next1D(r);
+    p.x = canonical_from_u64(a); // braced-init-list: left-to-right
+    p.y = canonical_from_u64(b);
     return p;
 }
 
@@ -555,8 +673,6 @@ struct Isect {
     float t;
     f3    n, p;
     int   material;
-    bool  unbounded; // on an unbounded shape (plane): outside the BVH, so the shadow ray's walk has
-                     // no leaves of its own origin (wide_any_packet)
 };
 
 // Shape-specific surface data for the final closest hit (identical arithmetic to the reference,
@@ -568,9 +684,13 @@ __device__ __forceinline__ Isect finish_hit(const Scene& sc, const Hit& h, const
     const uint32_t id   = h.code & CODE_MASK;
     is.t = h.t;
     is.p = ray_at(ray, h.t);
-    is.unbounded = kind == KIND_PLANE;
     if (kind == KIND_TRI) {
+        SP_TD(td_lines(TD_HIT, &sc.indices[3 * id], 12));
+        SP_TD(td_lines(TD_HIT, &sc.tri_material[id], 4));
         const uint32_t i0 = sc.indices[3 * id], i1 = sc.indices[3 * id + 1], i2 = sc.indices[3 * id + 2];
+        SP_TD(td_lines(TD_HIT, &sc.normals[3 * i0], 12));
+        SP_TD(td_lines(TD_HIT, &sc.normals[3 * i1], 12));
+        SP_TD(td_lines(TD_HIT, &sc.normals[3 * i2], 12));
         const f3 n0 = mk(sc.normals[3 * i0], sc.normals[3 * i0 + 1], sc.normals[3 * i0 + 2]);
         const f3 n1 = mk(sc.normals[3 * i1], sc.normals[3 * i1 + 1], sc.normals[3 * i1 + 2]);
         const f3 n2 = mk(sc.normals[3 * i2], sc.normals[3 * i2 + 1], sc.normals[3 * i2 + 2]);
@@ -624,6 +744,7 @@ __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, con
 // with prim_closest (their slot is ~0).
 __device__ __forceinline__ bool prim_closest_w(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h)
 {
+    SP_TD(td_lines(TD_TRI, &sc.wslot_tri[3 * slot], 48));
     const float4   q0   = sc.wslot_tri[3 * slot]; // p0 | code
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
@@ -645,6 +766,7 @@ __device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const R
                                          const float4* tris = nullptr)
 {
     const float4*  st   = tris ? tris : sc.slot_tri;
+    SP_TD(td_lines(tris ? TD_TRI : TD_BIN, &st[3 * slot], 48));
     const float4   q0   = st[3 * slot]; // p0 | code
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
@@ -791,6 +913,7 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
                                                float tmax, uint32_t filter = 0xffu)
 {
     const uint4*   np = sc.wnodes + 5 * (size_t)node;
+    SP_TD(td_lines(TD_NODE, np, 80));
     const uint4    w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
     const float    px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
     const float    sx = __uint_as_float((w0.w & 0xffu) << 23);
@@ -879,145 +1002,6 @@ __device__ __forceinline__ uint32_t key_mask(uint32_t m, uint32_t o)
     m = (o & 2u) ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
     m = (o & 4u) ? (((m & 0x0fu) << 4) | ((m >> 4) & 0x0fu)) : m;
     return m;
-}
-
-// ---------------------------------------------------------------- any-hit walk as one wave packet
-// DirectLighting's shadow rays of one 8x8 tile all end on the same light, so their walks over the
-// 8-wide BVH visit nearly the same nodes -- but each lane fetched them itself: five dwordx4 loads
-// per node, each a vector-L1 tag lookup per active lane (61 lookups per VMEM instruction in the
-// bunny frame, round 4), at 0.29 walk-step lane occupancy.  Here the wave walks ONE node sequence,
-// the union of its lanes' walks: the node index is wave-uniform, so the node (80 B) and the leaf
-// triangles (48 B each) are fetched once for the wave with scalar loads, and every lane box-tests
-// and triangle-tests its own ray.  A lane takes part in a node only if its own walk would visit
-// it -- its ray hit that node's box in the parent, and the parent's box before that (per-lane
-// child masks on the LDS stack) -- so each lane tests exactly the primitives its per-lane walk
-// (wide_any) would, and its answer, an OR over that set, is the same bit.  Lanes that found a hit
-// drop out; the walk ends when every lane has one or the union is exhausted.  Traversal order
-// follows the octant of the wave's first lane.  Incoherent packets (a tile straddling a
-// silhouette) make the union long: after SP_PACKET_BUDGET node steps the lanes still unresolved
-// finish with their own per-lane walks from the root (re-testing primitives does not change an OR).
-// Stack: per level, each lane's own inner-child mask (slot order) in row sp, and the wave's
-// pending group {child_base << 8 | union key mask} in row sp + depth / 2 (written alike by every
-// lane, read back with readfirstlane); needs the wide closest-hit stack layout (Scene::wide_closest).
-// SP_RENDER_PER_LANE_QUERIES (Scene::merge_queries = 0) keeps the per-lane walks, for comparison.
-#ifndef SP_PACKET_ANY
-#define SP_PACKET_ANY 0
-#endif
-#ifndef SP_PACKET_BUDGET
-#define SP_PACKET_BUDGET 0 // node steps before the per-lane fallback; 0 = none
-#endif
-typedef const __attribute__((address_space(4))) uint32_t cu32; // scalar (constant) loads, below too
-__device__ __forceinline__ uint4 uload4(cu32* q, int i) { return make_uint4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]); }
-__device__ __forceinline__ uint32_t ufirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-template <class T>
-__device__ __forceinline__ const T* uniform_ptr(const T* p)
-{
-    const uint64_t a = (uint64_t)(uintptr_t)p;
-    return (const T*)(uintptr_t)(((uint64_t)ufirst((uint32_t)(a >> 32)) << 32) | ufirst((uint32_t)a));
-}
-__device__ __forceinline__ bool wide_any_packet(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
-{
-    const f3       inv  = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    const uint32_t ou   = ufirst(dir_sign_bits(ray.d)); // the packet's visiting order
-    const int      half = st.depth >> 1;
-    uint32_t*      own  = st.s + st.lane;               // row e: own[e * 64]
-    uint32_t*      uni  = st.s + half * 64 + st.lane;   // row e: uni[e * 64]
-    int            sp   = 0;
-    uint32_t       node = 0;
-    bool           mine = true, hit = false;
-    int            steps = 0;
-    while (true) {
-#ifdef SP_WAVE_PROF
-        const uint64_t t_it = __builtin_amdgcn_s_memtime(); // region 7: any-hit walk steps
-#endif
-        cu32* np = (cu32*)uniform_ptr(sc.wnodes + 5 * (size_t)node);
-        const uint4 w0 = uload4(np, 0), w1 = uload4(np, 1), w2 = uload4(np, 2), w3 = uload4(np, 3), w4 = uload4(np, 4);
-        const float px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
-        const float sx = __uint_as_float((w0.w & 0xffu) << 23);
-        const float sy = __uint_as_float(((w0.w >> 8) & 0xffu) << 23);
-        const float sz = __uint_as_float(((w0.w >> 16) & 0xffu) << 23);
-        const uint32_t imask = w0.w >> 24;
-        const bool     live  = mine && !hit;
-        uint32_t       my_inner = 0, my_leaf = 0, u_inner = 0, u_leaf = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t meta  = ((k < 4 ? w1.z : w1.w) >> (8 * (k & 3))) & 0xffu;
-            const bool     inner = (imask >> k) & 1u;
-            if (!inner && meta == 0u) continue;
-            const int   h  = k >> 2;
-            const float lx = fma_f(ubyte(h ? w2.y : w2.x, k), sx, px);
-            const float ly = fma_f(ubyte(h ? w2.w : w2.z, k), sy, py);
-            const float lz = fma_f(ubyte(h ? w3.y : w3.x, k), sz, pz);
-            const float hx = fma_f(ubyte(h ? w3.w : w3.z, k), sx, px);
-            const float hy = fma_f(ubyte(h ? w4.y : w4.x, k), sy, py);
-            const float hz = fma_f(ubyte(h ? w4.w : w4.z, k), sz, pz);
-            float       t0;
-            const bool  b   = live && wbox(lx, ly, lz, hx, hy, hz, ray, inv, tmin, tmax, t0);
-            const bool  any = __ballot(b) != 0;
-            if (inner) { my_inner |= (b ? 1u : 0u) << k; u_inner |= (any ? 1u : 0u) << k; }
-            else { my_leaf |= (b ? 1u : 0u) << k; u_leaf |= (any ? 1u : 0u) << k; }
-        }
-        for (uint32_t m = u_leaf; m; m &= m - 1) {
-            const int      k    = __ffs(m) - 1;
-            const uint32_t meta = ((k < 4 ? w1.z : w1.w) >> (8 * (k & 3))) & 0xffu;
-            const uint32_t base = w1.y + (meta & 31u);
-            const bool     test = (my_leaf >> k) & 1u;
-            for (uint32_t j = 0; j < (meta >> 5); ++j) {
-                cu32* tp = (cu32*)uniform_ptr(sc.wslot_tri + 3 * (size_t)(base + j));
-                const uint4    a0 = uload4(tp, 0), a1 = uload4(tp, 1), a2 = uload4(tp, 2);
-                const uint32_t code = a0.w;
-                if ((code >> CODE_SHIFT) == KIND_TRI) {
-                    const float4 q0 = make_float4(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z), 0.0f);
-                    const float4 q1 = make_float4(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z), 0.0f);
-                    const float4 q2 = make_float4(__uint_as_float(a2.x), __uint_as_float(a2.y), __uint_as_float(a2.z), 0.0f);
-                    float t, be, ga;
-                    if (test && !hit && tri_hit(q0, q1, q2, ray, tmin, tmax, t, be, ga)) hit = true;
-                } else if (test && !hit) {
-                    hit = prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri);
-                }
-            }
-        }
-#ifdef SP_WAVE_PROF
-        wprof_end(7, t_it);
-#endif
-        if (__ballot(!hit) == 0) return true; // every lane of the packet is occluded
-        ++steps;
-        if (SP_PACKET_BUDGET > 0 && steps >= SP_PACKET_BUDGET) break;
-        if (u_inner) {
-            const uint32_t keys = key_mask(u_inner, ou);
-            const int      kf   = __ffs(keys) - 1;
-            const uint32_t rest = keys & (keys - 1);
-            if (rest) {
-                own[sp * 64] = my_inner;
-                uni[sp * 64] = (w1.x << 8) | rest;
-                ++sp;
-            }
-            const uint32_t slot = (uint32_t)kf ^ ou;
-            node = w1.x + slot;
-            mine = (my_inner >> slot) & 1u;
-            continue;
-        }
-        bool found = false;
-        while (sp > 0) { // next pending child some unresolved lane hit
-            const uint32_t e = ufirst(uni[(sp - 1) * 64]);
-            uint32_t       m = e & 0xffu;
-            const int      k = __ffs(m) - 1;
-            m &= m - 1;
-            const uint32_t slot = (uint32_t)k ^ ou;
-            const bool     me   = (own[(sp - 1) * 64] >> slot) & 1u;
-            if (m) uni[(sp - 1) * 64] = (e & ~0xffu) | m;
-            else --sp;
-            if (__ballot(me && !hit) == 0) continue; // nobody left who needs this subtree
-            node  = (e >> 8) + slot;
-            mine  = me;
-            found = true;
-            break;
-        }
-        if (!found) return hit;
-    }
-    // budget spent: the unresolved lanes walk on their own
-    if (!hit) hit = wide_any(sc, ray, tmin, tmax, st);
-    return hit;
 }
 
 // Closest hit over the 8-wide BVH: at each node the hit leaves' primitives are tested, the
@@ -1122,8 +1106,9 @@ __device__ __forceinline__ void mq_sync()
 #endif
 // The per-wave LDS rows a shared walk uses: L::O / D3 / T3 the any-hit rays (origin, direction,
 // t_min), L::AMAX their t_max, L::ANY their results; L::D1 / T1 the closest-hit rays (origin in
-// L::O too), L::BEST their u64 (t, wide slot) answers; L::TB the walking lanes' stack bounds and
-// queries, L::Q the queue (query r = owner lane | any-hit << 7), L::CNT its next unclaimed entry.
+// L::O too, or the camera's for a camera ray), L::BEST their u64 (t, wide slot) answers; L::TB the
+// walking lanes' stack bounds and queries, L::Q the queue (query r = owner lane | camera ray << 6 |
+// any-hit << 7), L::CNT its next unclaimed entry.
 // All lanes in integrate() call it; total = queries in m[L::Q..] (posted and synchronised by the
 // caller).  any_tmax: any-hit queries' t_max is in m[L::AMAX + owner]; else FLT_MAX (MIS rays).
 // ANY_ONLY: no closest-hit query is ever posted (the closest-hit code is not compiled).
@@ -1146,12 +1131,13 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
     f3       inv  = mk(0, 0, 0);
     uint32_t o    = 0, node = 0;
     float    tmin = 0.0f, amax = k_infinite;
-    bool     any  = false, has_node = false;
+    bool     any  = false, has_node = false, cam = false;
     int      own  = -1, sp = 0, bot = 0;
-    auto load = [&](uint32_t e) { // query e = owner | any << 6
+    auto load = [&](uint32_t e) { // query e = owner | any << 6 | camera ray << 7
         own   = (int)(e & 63u);
         any   = ANY_ONLY || (e & 64u) != 0u;
-        ray.o = mq_f3(m, L::O, own);
+        cam   = !ANY_ONLY && (e & 128u) != 0u;
+        ray.o = cam ? sc.camera.p : mq_f3(m, L::O, own);
         ray.d = mq_f3(m, any ? L::D3 : L::D1, own);
         tmin  = mq_f(m, (any ? L::T3 : L::T1) + own);
         amax  = (any && any_tmax) ? mq_f(m, L::AMAX + own) : k_infinite;
@@ -1160,9 +1146,9 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
     };
     auto take = [&](int qi) {
         const uint32_t e = qs[qi];
-        load((e & 63u) | ((e >> 1) & 64u));
+        load((e & 63u) | ((e >> 1) & 64u) | ((e << 1) & 128u));
         node = 0; has_node = true; sp = 0; bot = 0;
-        m[L::TB + lane] = ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
+        m[L::TB + lane] = ((uint32_t)own << 16) | (any ? 1u << 22 : 0u) | (cam ? 1u << 23 : 0u);
     };
     if (q < total) take(q);
     while (true) {
@@ -1231,7 +1217,8 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
                 }
             }
             if (!has_node && sp == bot) own = -1; // this lane's part of the query is done
-            m[L::TB + lane] = (uint32_t)sp | ((uint32_t)bot << 8) | ((uint32_t)(own & 63) << 16) | (any ? 1u << 22 : 0u);
+            m[L::TB + lane] = (uint32_t)sp | ((uint32_t)bot << 8) | ((uint32_t)(own & 63) << 16) | (any ? 1u << 22 : 0u) |
+                              (cam ? 1u << 23 : 0u);
 #ifdef SP_WAVE_PROF
             wprof_end(4, t_it);
 #endif
@@ -1261,11 +1248,11 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
                 const uint32_t e  = st.s[vb * 64 + vict];
                 const uint32_t dd = st.s[(vb + half) * 64 + vict];
                 m[L::TB + vict]   = (tb & ~0xff00u) | ((uint32_t)(vb + 1) << 8);
-                load(((tb >> 16) & 63u) | ((tb >> 16) & 64u));
+                load(((tb >> 16) & 63u) | ((tb >> 16) & 64u) | ((tb >> 16) & 128u));
                 st.s[st.lane]          = e; // the stolen group is this lane's whole stack
                 st.s[half * 64 + st.lane] = dd;
                 sp = 1; bot = 0; has_node = false;
-                m[L::TB + lane] = 1u | ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
+                m[L::TB + lane] = 1u | ((uint32_t)own << 16) | (any ? 1u << 22 : 0u) | (cam ? 1u << 23 : 0u);
             }
             mq_sync();
         }
@@ -1429,15 +1416,11 @@ __device__ __forceinline__ bool unbounded_any(const Scene& sc, const Ray& ray, f
     }
     return false;
 }
-template <bool PACKET = false>
 __device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
     if (unbounded_any(sc, ray, tmin, tmax)) return true;
     if (sc.n_nodes == 0) return false;
-    if (sc.wnodes) {
-        if (PACKET && sc.wide_closest && sc.merge_queries) return wide_any_packet(sc, ray, tmin, tmax, st);
-        return wide_any(sc, ray, tmin, tmax, st);
-    }
+    if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
     return sc.stackless ? bvh_any<true>(sc, ray, tmin, tmax, st) : bvh_any<false>(sc, ray, tmin, tmax, st);
 }
 
@@ -1707,10 +1690,9 @@ __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, floa
 }
 
 // Scene::intersect_p (base/Scene.h:79)
-template <bool PACKET = false>
 __device__ __forceinline__ bool scene_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
 {
-    return geometry_any<PACKET>(sc, ray, tmin, tmax, st) || lights_any(sc, ray, tmin, tmax, st);
+    return geometry_any(sc, ray, tmin, tmax, st) || lights_any(sc, ray, tmin, tmax, st);
 }
 
 // ------------------------------------------------------------------------------ sampling
@@ -2075,8 +2057,10 @@ __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPr
     r.pdf   = 0.0f;
     r.props = 0;
     if (wo.y == 0.0f) return r;
-    const float U2 = next1D<NT>(rng);
-    const float U1 = next1D<NT>(rng);
+    uint64_t u2, u1;
+    rng_raw2<NT>(rng, u2, u1); // U2 first, then U1
+    const float U2 = canonical_from_u64(u2);
+    const float U1 = canonical_from_u64(u1);
     P2          sl = beckmann_sample11_pre(p, U1, U2);
     const float tmp = p.cphi * sl.x - p.sphi * sl.y;
     sl.y            = p.sphi * sl.x + p.cphi * sl.y;
@@ -2497,13 +2481,12 @@ struct Ctx {
 #define SP_PROF(k, stmt) stmt
 #endif
 
-template <bool PACKET = false>
 __device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float tmax)
 {
     ++c.shadow;
     ++c.rays;
     bool hit;
-    SP_WPROF(3, hit = scene_any<PACKET>(c.sc, r, tmin, tmax, c.st));
+    SP_WPROF(3, hit = scene_any(c.sc, r, tmin, tmax, c.st));
     return hit;
 }
 
@@ -2542,17 +2525,7 @@ __device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
         rgb      f;
         SP_PROF(2, f = material_eval(c.sc, is.material, wo, wi, is.n, c.rng, c.q));
         bool vis = false;
-        if (!cblack(f)) {
-#if SP_PACKET_ANY == 2
-            // packet walks only when every lane's shadow ray leaves an unbounded shape (a floor
-            // plane): rays leaving BVH geometry each start inside their own leaves, and the union
-            // of those neighbourhoods makes the packet's node sequence long
-            if (__ballot(!is.unbounded) == 0) SP_PROF(3, vis = !occluded<true>(c, ls.ray, ls.tmin, ls.tmax));
-            else SP_PROF(3, vis = !occluded<false>(c, ls.ray, ls.tmin, ls.tmax));
-#else
-            SP_PROF(3, vis = !occluded<SP_PACKET_ANY != 0>(c, ls.ray, ls.tmin, ls.tmax));
-#endif
-        }
+        if (!cblack(f)) SP_PROF(3, vis = !occluded(c, ls.ray, ls.tmin, ls.tmax));
         if (vis) L = cadd(L, cdivs(cscale(cmul(f, ls.L), abs_f(dot(wi, is.n))), ls.pdf));
     }
     return L;
@@ -2781,6 +2754,7 @@ __device__ __forceinline__ void served_weights(const Material& m, f3 wo, uint64_
                                                float w[2])
 {
     Rng sr;
+    SP_TD(sr.td_cat = TD_SERVED);
     sr.base  = base;
     sr.cur   = cur;
     sr.idx   = idx;
@@ -2977,6 +2951,8 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
 #endif
     for (int depth = 0; depth < c.sc.max_depth; ++depth) {
         if (!__any(alive)) break;
+        // lock-step efficiency: wave bounce iterations (lines slot) and the lanes alive in them
+        SP_TD(td_add(TD_BOUNCE, 1, (uint64_t)__popcll(__ballot(alive))));
         MSample s;
         f3      wo  = mk(0, 0, 0), n = mk(0, 0, 0);
         bool    hit = false, pend = false;
@@ -3160,6 +3136,231 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
     }
     return L;
 }
+
+// PerspectiveCamera::generate_ray for sample i of pixel (px, py) (main.cpp:96-98; sp_mega.hpp)
+__device__ __forceinline__ Ray camera_ray(const Scene& sc, uint32_t px, uint32_t py, uint32_t seed2d, uint32_t i,
+                                          const Rsq& q)
+{
+    const float sx = rseq_component(seed2d, sc.alpha2_0, i);
+    const float sy = rseq_component(seed2d, sc.alpha2_1, i);
+    const float fx = (float)(int)px + sx;
+    const float fy = (float)(int)py + sy;
+    Ray         ray;
+    ray.o = sc.camera.p;
+    ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
+    return ray;
+}
+
+#ifndef SP_RRNEE_REGEN
+#define SP_RRNEE_REGEN 0
+#endif
+#if SP_MERGE_QUERIES
+// IterativeRRNEE over all of a pixel's samples with path regeneration: the same per-lane operations
+// as integrate_rrnee, but a lane whose path ends starts its pixel's next sample in the next bounce
+// iteration instead of idling until the wave's longest path of this sample has ended.  In lock step
+// only 0.70 of the lanes were alive per bounce iteration on elf (44.8 of 64; profiles/r05/traffic);
+// the served estimates and the merged walks filled some of those lanes, the per-lane code did not.
+// A pixel's samples still run one after the other on its own lane, so its stream words and its
+// running sum (image(p) += L, main.cpp:98) come in the reference's order: bit-identical.  The next
+// sample's camera ray joins the iteration's merged closest-hit pass (its trace(): intersect_lights
+// and the unbounded shapes by the lane, the BVH walk in the pass), like a bounce ray.
+__device__ __forceinline__ rgb integrate_rrnee_regen(Ctx& c, uint32_t px, uint32_t py, uint32_t seed2d, uint32_t spp)
+{
+    constexpr float rr_cut = 0.1f;
+    const bool mq = c.sc.merge_queries != 0 && c.sc.wide_closest != 0 && !c.sc.stackless;
+    uint32_t*  m  = srv_lds[threadIdx.x >> 6];
+    rgb        acc = mkc(0, 0, 0);
+    uint32_t   next = 1; // samples started
+    Ray        ray  = camera_ray(c.sc, px, py, seed2d, 0u, c.q);
+    rgb        throughput = mkc(1, 1, 1);
+    rgb        L          = mkc(0, 0, 0);
+    float      tmin = k_ray_epsilon, tmax = k_infinite;
+    int        depth  = 0;
+    bool       alive  = spp > 0 && c.sc.max_depth > 0;
+    bool       traced = false; // this bounce's closest hit came from the previous merged pass
+    Query      qr;
+    if (spp > 0 && c.sc.max_depth <= 0) next = spp; // no bounce at all: every sample is black
+    while (__any(alive)) {
+        SP_TD(td_add(TD_BOUNCE, 1, (uint64_t)__popcll(__ballot(alive))));
+        MSample s;
+        f3      wo  = mk(0, 0, 0), n = mk(0, 0, 0);
+        bool    hit = false, pend = false;
+        const bool was_alive = alive;
+        Rng     snap = c.rng;
+        bool    tail = false, post1 = false;
+        rgb     L_vis = mkc(0, 0, 0);
+        if (alive) {
+            rng_prepare(c.rng);
+            if (!traced) qr = trace(c, ray, tmin, tmax);
+            if (qr.geom) {
+                wo = neg(ray.d);
+                n  = qr.is.n;
+#if SP_SERVE_SAMPLE
+                const bool defer = c.sc.n_lights > 0 && material_has_rho(c.sc, qr.is.material);
+                if (defer) {
+                    rng_reserve(c.rng, 140);
+                    snap = c.rng;
+                    const Material& mm   = c.sc.materials[qr.is.material];
+                    const f3        wl   = to_onb(onb_from_v(n, c.q), wo);
+                    bool            spec = false;
+                    if (mm.kind == SP_MAT_CLEARCOAT) spec = next1D(c.rng) < fresnel_dielectric(wl.y, 1.0f, mm.coat_ior);
+                    if (spec) {
+                        c.rng = snap;
+                    } else {
+                        pend           = true;
+                        c.rng.srv_dc   = (wl.y == 0.0f) ? 0u : 32u;
+                        c.rng.srv_posA = c.rng.draws;
+                        c.rng.srv_pwA  = ((uint32_t)c.rng.cur << 16) | (uint32_t)c.rng.idx;
+                        rng_skip_reserved(c.rng, (int)c.rng.srv_dc + 3);
+                    }
+                }
+                if (!pend)
+#endif
+                s = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
+                if (pend) hit = true;
+                else if (s.pdf == 0.0f || cblack(s.color)) alive = false;
+                else hit = true;
+            } else {
+                if (qr.lh.hit) L = cadd(L, cmul(throughput, light_hit_L(c.sc, qr.lh, ray.d, c.q)));
+                alive = false;
+            }
+        }
+        for (int li = 0; li < c.sc.n_lights; ++li) {
+            LSample        ls;
+            bool           go = false, want = false;
+            const uint32_t rays0 = c.rays, shadow0 = c.shadow;
+#if SP_MQ_SHADOW
+            if (mq) {
+                go   = mis_light_part_mq(c, c.sc.lights[li], qr.is.p, n, ls, hit, m);
+                want = go && material_has_rho(c.sc, qr.is.material);
+            } else
+#endif
+            if (hit) {
+                go   = mis_light_part(c, c.sc.lights[li], qr.is.p, n, ls);
+                want = go && material_has_rho(c.sc, qr.is.material);
+            }
+            serve_rho(c, want, li == 0 && pend, (want || pend) ? qr.is.material : 0, n, wo);
+#if SP_SERVE_SAMPLE
+            if (li == 0 && pend) {
+                Rng ra      = snap;
+                ra.srv_on   = 1;
+                ra.srv_A    = true;
+                ra.srv_B    = false;
+                ra.srv_posA = c.rng.srv_posA;
+                ra.srv_dc   = c.rng.srv_dc;
+                s           = material_sample(c.sc, qr.is.material, wo, n, ra, c.q);
+                c.rng.srv_A = false;
+                if (s.pdf == 0.0f || cblack(s.color)) {
+                    ra.srv_on = 0;
+                    ra.srv_A  = false;
+                    c.rng     = ra;
+                    c.rays    = rays0;
+                    c.shadow  = shadow0;
+                    hit = go = alive = false;
+                }
+            }
+#endif
+            if (hit) {
+                rgb e = mkc(0, 0, 0);
+                rgb e_vis = mkc(0, 0, 0);
+                if (go && mq && li == c.sc.n_lights - 1)
+                    tail = mis_material_part_mq(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material, m, e, e_vis);
+                else if (go) e = mis_material_part(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material);
+                c.rng.srv_on = 0;
+                c.rng.srv_B  = false;
+                if (tail) L_vis = cadd(L, cmul(throughput, e_vis));
+                L = cadd(L, cmul(throughput, e));
+            }
+        }
+        if (hit) {
+            const f3    next_o = ray_at(ray, qr.is.t);
+            const f3    wi     = s.dir;
+            const float cosine = abs_f(dot(wi, n));
+            throughput         = cmul(throughput, cdivs(cscale(s.color, cosine), s.pdf));
+            if (depth >= c.sc.rr_depth) {
+                const float lum = luminance(throughput);
+                if (lum < rr_cut) {
+                    const float qv = std_max(0.05f, lum / rr_cut);
+                    if (next1D(c.rng) < qv) throughput = cdivs(throughput, qv);
+                    else alive = false;
+                }
+            }
+            ray.o = next_o;
+            ray.d = wi;
+            tmin  = ray_offset(cosine);
+            tmax  = k_infinite;
+        }
+        // the path ends in this iteration: no usable hit, Russian roulette, or max_depth reached
+        if (depth + 1 >= c.sc.max_depth) alive = false;
+        const bool ended = was_alive && !alive;
+        const bool regen = ended && next < spp;
+        if (regen) { // the pixel's next sample: its camera ray
+            ray  = camera_ray(c.sc, px, py, seed2d, next, c.q);
+            tmin = k_ray_epsilon;
+            tmax = k_infinite;
+        }
+        if (mq && ((alive && hit) || regen)) {
+            // the next closest hit (bounce or camera ray): trace()'s intersect_lights and unbounded
+            // shapes now, the BVH walk in the merged pass
+            ++c.rays;
+            qr.lh          = scene_intersect_lights(c.sc, ray, tmin, tmax, c.st);
+            const float tm = qr.lh.hit ? qr.lh.t : tmax;
+            const Hit   h0 = scene_intersect_unbounded(c.sc, ray, tmin, tm);
+            const int   ln = threadIdx.x & 63;
+            // a camera ray's origin is the camera's (queue bit 6): the shared origin slot keeps this
+            // lane's MIS ray, which starts at the hit point of the path just ended
+            if (!regen) mq_put3(m, MQ_O, ln, ray.o);
+            mq_put3(m, MQ_D1, ln, ray.d);
+            m[MQ_T1 + ln]              = __float_as_uint(tmin);
+            *mq_best<MqLayout>(m, ln) = ((unsigned long long)__float_as_uint(h0.t) << 32) | 0xffffffffull;
+            post1                      = true;
+        }
+        traced = false;
+        if (mq) {
+            const uint64_t m1 = __ballot(post1), m3 = __ballot(tail);
+            if ((m1 | m3) != 0ull) {
+                const int      ln = threadIdx.x & 63;
+                const uint64_t lt = (1ull << ln) - 1ull;
+                const int      n1 = __popcll(m1);
+                uint8_t*       qs = reinterpret_cast<uint8_t*>(m + MQ_Q);
+                if (post1) qs[__popcll(m1 & lt)] = (uint8_t)(ln | (regen ? 0x40 : 0));
+                if (tail) qs[n1 + __popcll(m3 & lt)] = (uint8_t)(ln | 0x80);
+                mq_sync();
+                SP_WPROF(5, mq_run<MqLayout>(c.sc, c.st, m, n1 + __popcll(m3)));
+                if (tail && !mis_ray_occluded(c, m)) L = L_vis;
+                if (post1) {
+                    const unsigned long long key = *mq_best<MqLayout>(m, ln);
+                    const uint32_t slot = (uint32_t)key;
+                    Hit h;
+                    if (slot == 0xffffffffu) {
+                        h = scene_intersect_unbounded(c.sc, ray, tmin, qr.lh.hit ? qr.lh.t : tmax);
+                    } else {
+                        h.t = k_infinite; h.code = 0xffffffffu; h.slot = 0xffffffffu;
+                        prim_closest_w(c.sc, slot, ray, tmin, h);
+                    }
+                    qr.geom = (h.code != 0xffffffffu);
+                    if (qr.geom) qr.is = finish_hit(c.sc, h, ray, c.q);
+                    traced = true;
+                }
+                mq_sync();
+            }
+        }
+        if (ended) {
+            acc = cadd(acc, L); // image(p) += integrate(...), in sample order
+            if (regen) {
+                ++next;
+                throughput = mkc(1, 1, 1);
+                L          = mkc(0, 0, 0);
+                depth      = 0;
+                alive      = true;
+            }
+        } else if (alive) {
+            ++depth;
+        }
+    }
+    return acc;
+}
+#endif
 #else
 // IntegratorIterativeRRNEE (Integrators/Integrator.cpp:550)
 __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)

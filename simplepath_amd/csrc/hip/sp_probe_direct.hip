@@ -3,6 +3,8 @@
 // render's tile does; a translation unit of their own so they compile beside the render kernels.
 #define SP_RNG_PF 0
 #define SP_RHO_TOUCH 1
+// two consecutive draws at an even stream position: one 16-byte load (sp_path.hpp rng_raw2)
+#define SP_RNG_PAIR 1
 #include "sp_mega.hpp"
 
 namespace spd {

@@ -303,25 +303,6 @@ def test_rrnee_clipped_border_tiles_bitexact(scene_dir, scene, w, h, spp):
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32)), rel_l2(g, c)
 
 
-@pytest.mark.parametrize("scene,w,h,spp", [("bunny.sp", 64, 40, 3), ("bunny_scan.sp", 72, 48, 2),
-                                           ("material_spheres.sp", 24, 48, 2), ("material_spheres_ibl.sp", 24, 48, 2),
-                                           ("lucy_small.sp", 40, 56, 2), ("elf_small.sp", 37, 21, 2),
-                                           ("closed_room.sp", 16, 16, 2)])
-@pytest.mark.parametrize("pipeline", ["megakernel", "chunks"])
-def test_direct_packet_shadow_walks_equal_per_lane(scene_dir, scene, w, h, spp, pipeline):
-    # DirectLighting's shadow rays walk the 8-wide BVH as one wave packet on SAH scenes (sp_path.hpp
-    # wide_any_packet: wave-uniform node sequence, scalar node / triangle fetches, each lane testing
-    # only the nodes its own walk would visit); SP_RENDER_PER_LANE_QUERIES keeps the per-lane walks.
-    # Any-hit answers are an OR over the same primitives: bit-identical images and identical counts.
-    s = load(scene_dir, scene, w, h, bvh=0)
-    a, ast = sp.render_tiles(s, "direct_lighting", spp, pipeline=pipeline)
-    b, bst = sp.render_tiles(s, "direct_lighting", spp, pipeline=pipeline, per_lane_queries=True)
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), rel_l2(a, b)
-    assert (ast.rays, ast.shadow_rays, ast.samples, ast.rng_draws) == (bst.rays, bst.shadow_rays, bst.samples, bst.rng_draws)
-    c, _ = _oracle.render(s, sp.string_to_integrator_type("direct_lighting"), spp, variant="spm")
-    assert rel_l2(a, c) < REL_L2_TOL
-
-
 @pytest.mark.parametrize("scene,w,h,spp", [("elf_small.sp", 40, 56, 3), ("elf_small.sp", 70, 35, 2),
                                            ("material_spheres.sp", 24, 48, 3), ("material_spheres_ibl.sp", 24, 48, 3),
                                            ("bunny.sp", 64, 40, 2), ("lucy_small.sp", 40, 56, 2),
