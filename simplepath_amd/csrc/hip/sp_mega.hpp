@@ -85,12 +85,6 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
                 c.deep    = args.deep + gwave * 64 + lane;
                 c.dstride = args.deep_stride;
             }
-#if SP_SERVE_RHO && SP_MERGE_QUERIES
-            if constexpr (INTEG == SP_INTEGRATOR_ITERATIVE_RRNEE && SP_RRNEE_REGEN) {
-                // every sample of the pixel, paths regenerated as they end (sp_path.hpp)
-                SP_WPROF(0, acc = integrate_rrnee_regen(c, px, py, seed2d, args.spp));
-            } else
-#endif
             for (uint32_t i = 0; i < args.spp; ++i) {
                 rng_prepare(rng);
                 // RSequenceSampler::get_next_2D (math/Sampler.h:158) with count i

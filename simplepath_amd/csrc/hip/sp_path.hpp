@@ -1106,9 +1106,8 @@ __device__ __forceinline__ void mq_sync()
 #endif
 // The per-wave LDS rows a shared walk uses: L::O / D3 / T3 the any-hit rays (origin, direction,
 // t_min), L::AMAX their t_max, L::ANY their results; L::D1 / T1 the closest-hit rays (origin in
-// L::O too, or the camera's for a camera ray), L::BEST their u64 (t, wide slot) answers; L::TB the
-// walking lanes' stack bounds and queries, L::Q the queue (query r = owner lane | camera ray << 6 |
-// any-hit << 7), L::CNT its next unclaimed entry.
+// L::O too), L::BEST their u64 (t, wide slot) answers; L::TB the walking lanes' stack bounds and
+// queries, L::Q the queue (query r = owner lane | any-hit << 7), L::CNT its next unclaimed entry.
 // All lanes in integrate() call it; total = queries in m[L::Q..] (posted and synchronised by the
 // caller).  any_tmax: any-hit queries' t_max is in m[L::AMAX + owner]; else FLT_MAX (MIS rays).
 // ANY_ONLY: no closest-hit query is ever posted (the closest-hit code is not compiled).
@@ -1131,13 +1130,12 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
     f3       inv  = mk(0, 0, 0);
     uint32_t o    = 0, node = 0;
     float    tmin = 0.0f, amax = k_infinite;
-    bool     any  = false, has_node = false, cam = false;
+    bool     any  = false, has_node = false;
     int      own  = -1, sp = 0, bot = 0;
-    auto load = [&](uint32_t e) { // query e = owner | any << 6 | camera ray << 7
+    auto load = [&](uint32_t e) { // query e = owner | any << 6
         own   = (int)(e & 63u);
         any   = ANY_ONLY || (e & 64u) != 0u;
-        cam   = !ANY_ONLY && (e & 128u) != 0u;
-        ray.o = cam ? sc.camera.p : mq_f3(m, L::O, own);
+        ray.o = mq_f3(m, L::O, own);
         ray.d = mq_f3(m, any ? L::D3 : L::D1, own);
         tmin  = mq_f(m, (any ? L::T3 : L::T1) + own);
         amax  = (any && any_tmax) ? mq_f(m, L::AMAX + own) : k_infinite;
@@ -1146,9 +1144,9 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
     };
     auto take = [&](int qi) {
         const uint32_t e = qs[qi];
-        load((e & 63u) | ((e >> 1) & 64u) | ((e << 1) & 128u));
+        load((e & 63u) | ((e >> 1) & 64u));
         node = 0; has_node = true; sp = 0; bot = 0;
-        m[L::TB + lane] = ((uint32_t)own << 16) | (any ? 1u << 22 : 0u) | (cam ? 1u << 23 : 0u);
+        m[L::TB + lane] = ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
     };
     if (q < total) take(q);
     while (true) {
@@ -1217,8 +1215,7 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
                 }
             }
             if (!has_node && sp == bot) own = -1; // this lane's part of the query is done
-            m[L::TB + lane] = (uint32_t)sp | ((uint32_t)bot << 8) | ((uint32_t)(own & 63) << 16) | (any ? 1u << 22 : 0u) |
-                              (cam ? 1u << 23 : 0u);
+            m[L::TB + lane] = (uint32_t)sp | ((uint32_t)bot << 8) | ((uint32_t)(own & 63) << 16) | (any ? 1u << 22 : 0u);
 #ifdef SP_WAVE_PROF
             wprof_end(4, t_it);
 #endif
@@ -1248,11 +1245,11 @@ __device__ __forceinline__ void mq_run(const Scene& sc, Stack st, uint32_t* m, i
                 const uint32_t e  = st.s[vb * 64 + vict];
                 const uint32_t dd = st.s[(vb + half) * 64 + vict];
                 m[L::TB + vict]   = (tb & ~0xff00u) | ((uint32_t)(vb + 1) << 8);
-                load(((tb >> 16) & 63u) | ((tb >> 16) & 64u) | ((tb >> 16) & 128u));
+                load(((tb >> 16) & 63u) | ((tb >> 16) & 64u));
                 st.s[st.lane]          = e; // the stolen group is this lane's whole stack
                 st.s[half * 64 + st.lane] = dd;
                 sp = 1; bot = 0; has_node = false;
-                m[L::TB + lane] = 1u | ((uint32_t)own << 16) | (any ? 1u << 22 : 0u) | (cam ? 1u << 23 : 0u);
+                m[L::TB + lane] = 1u | ((uint32_t)own << 16) | (any ? 1u << 22 : 0u);
             }
             mq_sync();
         }
@@ -3137,230 +3134,6 @@ __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
     return L;
 }
 
-// PerspectiveCamera::generate_ray for sample i of pixel (px, py) (main.cpp:96-98; sp_mega.hpp)
-__device__ __forceinline__ Ray camera_ray(const Scene& sc, uint32_t px, uint32_t py, uint32_t seed2d, uint32_t i,
-                                          const Rsq& q)
-{
-    const float sx = rseq_component(seed2d, sc.alpha2_0, i);
-    const float sy = rseq_component(seed2d, sc.alpha2_1, i);
-    const float fx = (float)(int)px + sx;
-    const float fy = (float)(int)py + sy;
-    Ray         ray;
-    ray.o = sc.camera.p;
-    ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
-    return ray;
-}
-
-#ifndef SP_RRNEE_REGEN
-#define SP_RRNEE_REGEN 0
-#endif
-#if SP_MERGE_QUERIES
-// IterativeRRNEE over all of a pixel's samples with path regeneration: the same per-lane operations
-// as integrate_rrnee, but a lane whose path ends starts its pixel's next sample in the next bounce
-// iteration instead of idling until the wave's longest path of this sample has ended.  In lock step
-// only 0.70 of the lanes were alive per bounce iteration on elf (44.8 of 64; profiles/r05/traffic);
-// the served estimates and the merged walks filled some of those lanes, the per-lane code did not.
-// A pixel's samples still run one after the other on its own lane, so its stream words and its
-// running sum (image(p) += L, main.cpp:98) come in the reference's order: bit-identical.  The next
-// sample's camera ray joins the iteration's merged closest-hit pass (its trace(): intersect_lights
-// and the unbounded shapes by the lane, the BVH walk in the pass), like a bounce ray.
-__device__ __forceinline__ rgb integrate_rrnee_regen(Ctx& c, uint32_t px, uint32_t py, uint32_t seed2d, uint32_t spp)
-{
-    constexpr float rr_cut = 0.1f;
-    const bool mq = c.sc.merge_queries != 0 && c.sc.wide_closest != 0 && !c.sc.stackless;
-    uint32_t*  m  = srv_lds[threadIdx.x >> 6];
-    rgb        acc = mkc(0, 0, 0);
-    uint32_t   next = 1; // samples started
-    Ray        ray  = camera_ray(c.sc, px, py, seed2d, 0u, c.q);
-    rgb        throughput = mkc(1, 1, 1);
-    rgb        L          = mkc(0, 0, 0);
-    float      tmin = k_ray_epsilon, tmax = k_infinite;
-    int        depth  = 0;
-    bool       alive  = spp > 0 && c.sc.max_depth > 0;
-    bool       traced = false; // this bounce's closest hit came from the previous merged pass
-    Query      qr;
-    if (spp > 0 && c.sc.max_depth <= 0) next = spp; // no bounce at all: every sample is black
-    while (__any(alive)) {
-        SP_TD(td_add(TD_BOUNCE, 1, (uint64_t)__popcll(__ballot(alive))));
-        MSample s;
-        f3      wo  = mk(0, 0, 0), n = mk(0, 0, 0);
-        bool    hit = false, pend = false;
-        const bool was_alive = alive;
-        Rng     snap = c.rng;
-        bool    tail = false, post1 = false;
-        rgb     L_vis = mkc(0, 0, 0);
-        if (alive) {
-            rng_prepare(c.rng);
-            if (!traced) qr = trace(c, ray, tmin, tmax);
-            if (qr.geom) {
-                wo = neg(ray.d);
-                n  = qr.is.n;
-#if SP_SERVE_SAMPLE
-                const bool defer = c.sc.n_lights > 0 && material_has_rho(c.sc, qr.is.material);
-                if (defer) {
-                    rng_reserve(c.rng, 140);
-                    snap = c.rng;
-                    const Material& mm   = c.sc.materials[qr.is.material];
-                    const f3        wl   = to_onb(onb_from_v(n, c.q), wo);
-                    bool            spec = false;
-                    if (mm.kind == SP_MAT_CLEARCOAT) spec = next1D(c.rng) < fresnel_dielectric(wl.y, 1.0f, mm.coat_ior);
-                    if (spec) {
-                        c.rng = snap;
-                    } else {
-                        pend           = true;
-                        c.rng.srv_dc   = (wl.y == 0.0f) ? 0u : 32u;
-                        c.rng.srv_posA = c.rng.draws;
-                        c.rng.srv_pwA  = ((uint32_t)c.rng.cur << 16) | (uint32_t)c.rng.idx;
-                        rng_skip_reserved(c.rng, (int)c.rng.srv_dc + 3);
-                    }
-                }
-                if (!pend)
-#endif
-                s = material_sample(c.sc, qr.is.material, wo, n, c.rng, c.q);
-                if (pend) hit = true;
-                else if (s.pdf == 0.0f || cblack(s.color)) alive = false;
-                else hit = true;
-            } else {
-                if (qr.lh.hit) L = cadd(L, cmul(throughput, light_hit_L(c.sc, qr.lh, ray.d, c.q)));
-                alive = false;
-            }
-        }
-        for (int li = 0; li < c.sc.n_lights; ++li) {
-            LSample        ls;
-            bool           go = false, want = false;
-            const uint32_t rays0 = c.rays, shadow0 = c.shadow;
-#if SP_MQ_SHADOW
-            if (mq) {
-                go   = mis_light_part_mq(c, c.sc.lights[li], qr.is.p, n, ls, hit, m);
-                want = go && material_has_rho(c.sc, qr.is.material);
-            } else
-#endif
-            if (hit) {
-                go   = mis_light_part(c, c.sc.lights[li], qr.is.p, n, ls);
-                want = go && material_has_rho(c.sc, qr.is.material);
-            }
-            serve_rho(c, want, li == 0 && pend, (want || pend) ? qr.is.material : 0, n, wo);
-#if SP_SERVE_SAMPLE
-            if (li == 0 && pend) {
-                Rng ra      = snap;
-                ra.srv_on   = 1;
-                ra.srv_A    = true;
-                ra.srv_B    = false;
-                ra.srv_posA = c.rng.srv_posA;
-                ra.srv_dc   = c.rng.srv_dc;
-                s           = material_sample(c.sc, qr.is.material, wo, n, ra, c.q);
-                c.rng.srv_A = false;
-                if (s.pdf == 0.0f || cblack(s.color)) {
-                    ra.srv_on = 0;
-                    ra.srv_A  = false;
-                    c.rng     = ra;
-                    c.rays    = rays0;
-                    c.shadow  = shadow0;
-                    hit = go = alive = false;
-                }
-            }
-#endif
-            if (hit) {
-                rgb e = mkc(0, 0, 0);
-                rgb e_vis = mkc(0, 0, 0);
-                if (go && mq && li == c.sc.n_lights - 1)
-                    tail = mis_material_part_mq(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material, m, e, e_vis);
-                else if (go) e = mis_material_part(c, c.sc.lights[li], ls, qr.is.p, n, wo, qr.is.material);
-                c.rng.srv_on = 0;
-                c.rng.srv_B  = false;
-                if (tail) L_vis = cadd(L, cmul(throughput, e_vis));
-                L = cadd(L, cmul(throughput, e));
-            }
-        }
-        if (hit) {
-            const f3    next_o = ray_at(ray, qr.is.t);
-            const f3    wi     = s.dir;
-            const float cosine = abs_f(dot(wi, n));
-            throughput         = cmul(throughput, cdivs(cscale(s.color, cosine), s.pdf));
-            if (depth >= c.sc.rr_depth) {
-                const float lum = luminance(throughput);
-                if (lum < rr_cut) {
-                    const float qv = std_max(0.05f, lum / rr_cut);
-                    if (next1D(c.rng) < qv) throughput = cdivs(throughput, qv);
-                    else alive = false;
-                }
-            }
-            ray.o = next_o;
-            ray.d = wi;
-            tmin  = ray_offset(cosine);
-            tmax  = k_infinite;
-        }
-        // the path ends in this iteration: no usable hit, Russian roulette, or max_depth reached
-        if (depth + 1 >= c.sc.max_depth) alive = false;
-        const bool ended = was_alive && !alive;
-        const bool regen = ended && next < spp;
-        if (regen) { // the pixel's next sample: its camera ray
-            ray  = camera_ray(c.sc, px, py, seed2d, next, c.q);
-            tmin = k_ray_epsilon;
-            tmax = k_infinite;
-        }
-        if (mq && ((alive && hit) || regen)) {
-            // the next closest hit (bounce or camera ray): trace()'s intersect_lights and unbounded
-            // shapes now, the BVH walk in the merged pass
-            ++c.rays;
-            qr.lh          = scene_intersect_lights(c.sc, ray, tmin, tmax, c.st);
-            const float tm = qr.lh.hit ? qr.lh.t : tmax;
-            const Hit   h0 = scene_intersect_unbounded(c.sc, ray, tmin, tm);
-            const int   ln = threadIdx.x & 63;
-            // a camera ray's origin is the camera's (queue bit 6): the shared origin slot keeps this
-            // lane's MIS ray, which starts at the hit point of the path just ended
-            if (!regen) mq_put3(m, MQ_O, ln, ray.o);
-            mq_put3(m, MQ_D1, ln, ray.d);
-            m[MQ_T1 + ln]              = __float_as_uint(tmin);
-            *mq_best<MqLayout>(m, ln) = ((unsigned long long)__float_as_uint(h0.t) << 32) | 0xffffffffull;
-            post1                      = true;
-        }
-        traced = false;
-        if (mq) {
-            const uint64_t m1 = __ballot(post1), m3 = __ballot(tail);
-            if ((m1 | m3) != 0ull) {
-                const int      ln = threadIdx.x & 63;
-                const uint64_t lt = (1ull << ln) - 1ull;
-                const int      n1 = __popcll(m1);
-                uint8_t*       qs = reinterpret_cast<uint8_t*>(m + MQ_Q);
-                if (post1) qs[__popcll(m1 & lt)] = (uint8_t)(ln | (regen ? 0x40 : 0));
-                if (tail) qs[n1 + __popcll(m3 & lt)] = (uint8_t)(ln | 0x80);
-                mq_sync();
-                SP_WPROF(5, mq_run<MqLayout>(c.sc, c.st, m, n1 + __popcll(m3)));
-                if (tail && !mis_ray_occluded(c, m)) L = L_vis;
-                if (post1) {
-                    const unsigned long long key = *mq_best<MqLayout>(m, ln);
-                    const uint32_t slot = (uint32_t)key;
-                    Hit h;
-                    if (slot == 0xffffffffu) {
-                        h = scene_intersect_unbounded(c.sc, ray, tmin, qr.lh.hit ? qr.lh.t : tmax);
-                    } else {
-                        h.t = k_infinite; h.code = 0xffffffffu; h.slot = 0xffffffffu;
-                        prim_closest_w(c.sc, slot, ray, tmin, h);
-                    }
-                    qr.geom = (h.code != 0xffffffffu);
-                    if (qr.geom) qr.is = finish_hit(c.sc, h, ray, c.q);
-                    traced = true;
-                }
-                mq_sync();
-            }
-        }
-        if (ended) {
-            acc = cadd(acc, L); // image(p) += integrate(...), in sample order
-            if (regen) {
-                ++next;
-                throughput = mkc(1, 1, 1);
-                L          = mkc(0, 0, 0);
-                depth      = 0;
-                alive      = true;
-            }
-        } else if (alive) {
-            ++depth;
-        }
-    }
-    return acc;
-}
-#endif
 #else
 // IntegratorIterativeRRNEE (Integrators/Integrator.cpp:550)
 __device__ __forceinline__ rgb integrate_rrnee(Ctx& c, Ray ray)
