@@ -2,9 +2,13 @@
 // No RNG draw-ahead window here, but the glossy estimate's words are touched in advance
 // (sp_path.hpp SP_RHO_TOUCH): 2762 vs 2720 Mrays/s with the window of 2 (profiles/r02/s5).
 #define SP_RNG_PF 0
+#ifndef SP_RHO_TOUCH
 #define SP_RHO_TOUCH 1
+#endif
 // two consecutive draws at an even stream position: one 16-byte load (sp_path.hpp rng_raw2)
+#ifndef SP_RNG_PAIR
 #define SP_RNG_PAIR 1
+#endif
 #include "sp_mega.hpp"
 
 namespace spd {

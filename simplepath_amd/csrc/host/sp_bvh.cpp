@@ -8,7 +8,6 @@
 #include "sp_host.hpp"
 
 #include <cstdio>
-#include <cstdlib>
 
 #include <stdexcept>
 #include <cstring>
