@@ -718,10 +718,10 @@ __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, con
 {
     const float4*  st   = tris ? tris : sc.slot_tri;
     const float4   q0   = st[3 * slot]; // p0 | code
+    const float4   q1 = st[3 * slot + 1], q2 = st[3 * slot + 2]; // with q0: one memory latency (SP_TRI_EAGER)
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     if (kind == KIND_TRI) {
-        const float4 q1 = st[3 * slot + 1], q2 = st[3 * slot + 2];
         float t, be, ga;
         if (tri_hit(q0, q1, q2, ray, tmin, h.t, t, be, ga)) {
             h.t = t; h.code = code; h.beta = be; h.gamma = ga;
@@ -746,12 +746,12 @@ __device__ __forceinline__ bool prim_closest_w(const Scene& sc, uint32_t slot, c
 {
     SP_TD(td_lines(TD_TRI, &sc.wslot_tri[3 * slot], 48));
     const float4   q0   = sc.wslot_tri[3 * slot]; // p0 | code
+    const float4   q1 = sc.wslot_tri[3 * slot + 1], q2 = sc.wslot_tri[3 * slot + 2]; // issued with q0
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     float          t, be = 0.0f, ga = 0.0f;
     bool           hit;
     if (kind == KIND_TRI) {
-        const float4 q1 = sc.wslot_tri[3 * slot + 1], q2 = sc.wslot_tri[3 * slot + 2];
         hit = tri_hit(q0, q1, q2, ray, tmin, h.t, t, be, ga);
     } else {
         const Shape& s = sc.shapes[code & CODE_MASK];
@@ -768,10 +768,10 @@ __device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const R
     const float4*  st   = tris ? tris : sc.slot_tri;
     SP_TD(td_lines(tris ? TD_TRI : TD_BIN, &st[3 * slot], 48));
     const float4   q0   = st[3 * slot]; // p0 | code
+    const float4   q1 = st[3 * slot + 1], q2 = st[3 * slot + 2]; // issued with q0
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     if (kind == KIND_TRI) {
-        const float4 q1 = st[3 * slot + 1], q2 = st[3 * slot + 2];
         float t, be, ga;
         return tri_hit(q0, q1, q2, ray, tmin, tmax, t, be, ga);
     }
