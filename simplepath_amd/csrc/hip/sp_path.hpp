@@ -951,8 +951,14 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
 }
 
 __device__ __forceinline__ uint32_t key_mask(uint32_t m, uint32_t o);
-__device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+// occ (walk cache, SP_OCC_CACHE): the wide slot of the primitive that occluded this lane's previous
+// shadow ray.  It is tested first; if it occludes this ray too, the answer (an OR over every
+// primitive the ray meets in [tmin, tmax]) is true without a walk.  A hit found by the walk
+// becomes the new cached occluder.  Same answer either way: only which primitives are tested changes.
+__device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st,
+                                         uint32_t* occ = nullptr)
 {
+    if (occ && *occ != 0xffffffffu && prim_any(sc, *occ, ray, tmin, tmax, sc.wslot_tri)) return true;
     const f3       inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     const uint32_t o   = dir_sign_bits(ray.d);
     int            sp  = 0;
@@ -970,7 +976,11 @@ __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float 
             const uint32_t meta = ((k < 4 ? wh.meta_lo : wh.meta_hi) >> (8 * (k & 3))) & 0xffu;
             const uint32_t base = wh.leaf_base + (meta & 31u);
             for (uint32_t j = 0; j < (meta >> 5); ++j)
-                if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) { SP_WPROF_ANY; return true; }
+                if (prim_any(sc, base + j, ray, tmin, tmax, sc.wslot_tri)) {
+                    SP_WPROF_ANY;
+                    if (occ) *occ = base + j;
+                    return true;
+                }
         }
         SP_WPROF_ANY;
         if (wh.inner) {
@@ -1413,11 +1423,12 @@ __device__ __forceinline__ bool unbounded_any(const Scene& sc, const Ray& ray, f
     }
     return false;
 }
-__device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+__device__ __forceinline__ bool geometry_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st,
+                                             uint32_t* occ = nullptr)
 {
     if (unbounded_any(sc, ray, tmin, tmax)) return true;
     if (sc.n_nodes == 0) return false;
-    if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st);
+    if (sc.wnodes) return wide_any(sc, ray, tmin, tmax, st, occ);
     return sc.stackless ? bvh_any<true>(sc, ray, tmin, tmax, st) : bvh_any<false>(sc, ray, tmin, tmax, st);
 }
 
@@ -1687,9 +1698,10 @@ __device__ __forceinline__ bool lights_any(const Scene& sc, const Ray& ray, floa
 }
 
 // Scene::intersect_p (base/Scene.h:79)
-__device__ __forceinline__ bool scene_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st)
+__device__ __forceinline__ bool scene_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st,
+                                          uint32_t* occ = nullptr)
 {
-    return geometry_any(sc, ray, tmin, tmax, st) || lights_any(sc, ray, tmin, tmax, st);
+    return geometry_any(sc, ray, tmin, tmax, st, occ) || lights_any(sc, ray, tmin, tmax, st);
 }
 
 // ------------------------------------------------------------------------------ sampling
@@ -2453,12 +2465,20 @@ __device__ __forceinline__ float light_pdf(const Scene& sc, const Light& l, f3 o
 }
 
 // ============================================================================ integrators
+#ifndef SP_OCC_CACHE
+#define SP_OCC_CACHE 1
+#endif
 struct Ctx {
     const Scene& sc;
     Rng&         rng;
     const Rsq&   q;
     Stack        st;
     uint32_t     rays, shadow;
+    // occluder cache (SP_OCC_CACHE): the wide slot of this lane's last occluder, tried first by the
+    // next shadow walk; a pixel's samples run on one lane, so the previous sample's occluder is the
+    // likeliest (~0: none).  Measured: elf 1024^2 @ 16 spp +1.8 %, bunny and lucy level; the same
+    // cache for closest hits (the previous hit tested first to lower t_max) lost 1 % on lucy.
+    uint32_t     occ_slot = 0xffffffffu;
     // recursive integrators with max_depth > MAX_RECURSION: per-level records in global memory,
     // record k of this lane at deep[k * dstride] (level-major, lanes contiguous)
     float*       deep    = nullptr;
@@ -2483,7 +2503,7 @@ __device__ __forceinline__ bool occluded(Ctx& c, const Ray& r, float tmin, float
     ++c.shadow;
     ++c.rays;
     bool hit;
-    SP_WPROF(3, hit = scene_any(c.sc, r, tmin, tmax, c.st));
+    SP_WPROF(3, hit = scene_any(c.sc, r, tmin, tmax, c.st, SP_OCC_CACHE ? &c.occ_slot : nullptr));
     return hit;
 }
 
