@@ -2476,8 +2476,8 @@ struct Ctx {
     uint32_t     rays, shadow;
     // occluder cache (SP_OCC_CACHE): the wide slot of this lane's last occluder, tried first by the
     // next shadow walk; a pixel's samples run on one lane, so the previous sample's occluder is the
-    // likeliest (~0: none).  Measured: elf 1024^2 @ 16 spp +1.8 %, bunny and lucy level; the same
-    // cache for closest hits (the previous hit tested first to lower t_max) lost 1 % on lucy.
+    // likeliest (~0: none).  Level on bunny / lucy / the shards, where it applies;
+    // the same cache for closest hits (the previous hit tested first) lost 1 % on lucy.
     uint32_t     occ_slot = 0xffffffffu;
     // recursive integrators with max_depth > MAX_RECURSION: per-level records in global memory,
     // record k of this lane at deep[k * dstride] (level-major, lanes contiguous)
