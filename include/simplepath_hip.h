@@ -210,8 +210,8 @@ typedef struct sp_render_params {
     /* ---- ABI 5 ---- */
     float          tile_order_factor; /* megakernel tile order (DirectLighting, IterativeRRNEE): 0 =
                                          automatic (a one-sample probe times every tile; tiles
-                                         slower than 2x the mean go first, then those slower than
-                                         1x, 0.5x, ... the mean; from 6 tiles per wave and 128 spp,
+                                         slower than 2x the mean go first, then 24 cost classes a
+                                         quarter octave apart; from 6 tiles per wave and 128 spp,
                                          IterativeRRNEE from 4 tiles per wave and 16 spp);
                                          > 0: with this factor whenever it can apply; < 0: queue
                                          order.  It cannot apply, and the frame renders in queue
@@ -219,9 +219,11 @@ typedef struct sp_render_params {
                                          run (wavefront, sample chunks), when n_tiles is at most
                                          the persistent waves (each wave takes one tile), or for
                                          an integrator without a probe kernel (BruteForce*,
-                                         Whitted, Mandelbrot).  For a caller's tile list each
-                                         tile's own probe time is its estimate; for a whole frame
-                                         it is blended with its image neighbours'.                  */
+                                         Whitted, Mandelbrot).  A tile's estimate is its probe time
+                                         blended with its image neighbours' for a whole frame or a
+                                         host list in image order with a constant stride (a rank's
+                                         interleaved shard); any other list uses each tile's own
+                                         probe time.                                                  */
     int32_t        reserved[2];       /* must be 0                                                  */
 } sp_render_params;
 

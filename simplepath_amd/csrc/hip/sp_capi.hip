@@ -21,7 +21,7 @@ hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
 size_t     render_static_lds(int integ, int variant);
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, bool smooth, int32_t* order,
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
                              hipStream_t stream);
 bool       has_probe(int integ);
 hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
@@ -973,6 +973,19 @@ static ChunkPlan chunk_plan(const sp_scene* s, int64_t n_tiles, uint32_t spp, in
     return c;
 }
 
+// Queue neighbours of the tile-order kernel's cost estimate (sp_mega.hip tile_est): > 0 the queue
+// offset of the tile below (left / right at +-1), -1 left / right only, 0 none.
+static int order_neighbours(const sp_render_params* p, bool listed, int64_t n_tiles, int32_t tiles_x)
+{
+    if (!listed) return tiles_x;
+    if (!p->tile_ids || n_tiles < 2) return 0;
+    const int64_t k = (int64_t)p->tile_ids[1] - p->tile_ids[0];
+    if (k <= 0) return 0;
+    for (int64_t i = 2; i < n_tiles; ++i)
+        if ((int64_t)p->tile_ids[i] - p->tile_ids[i - 1] != k) return 0;
+    return (tiles_x % k == 0) ? (int)(tiles_x / k) : -1;
+}
+
 static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_out, sp_render_stats* stats)
 {
     if (!s || !p || !d_out) return fail(SP_ERR_ARG, "null argument");
@@ -1360,9 +1373,11 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
             SP_HIP(spd::launch_probe(sc_run, pr, integ, variant, blocks, lds_bytes, stream));
-            // cost estimates blended with queue neighbours only for a whole frame, where those are
-            // the tiles left and right (a caller's list may put unrelated tiles side by side)
-            SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, !listed, s->d_order, stream));
+            // cost estimates blended with their queue neighbours only where those are image
+            // neighbours: a whole frame, or a host list in image order with a constant stride (the
+            // bench's list, a rank's interleaved shard); any other list keeps each tile's own time
+            SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, order_neighbours(p, listed, n_tiles, a.tiles_x),
+                                          s->d_order, stream));
             SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
             a.order = s->d_order;
             launches += 2;

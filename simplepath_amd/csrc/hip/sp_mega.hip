@@ -48,39 +48,50 @@ hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int 
 // the last 15 % of the span ran below full occupancy, 9 % of the frame).  A probe pass renders
 // one sample of every tile (sp_probe_kernel with spp = 1: the render's code writing tile times
 // instead of radiance; the render re-seeds every pixel's stream) and times each tile; this kernel
-// then orders the queue by cost class: the tiles whose probe time exceeds `factor` x the mean
-// first, then those above factor / 2, factor / 4, ... x the mean (SP_TILE_CLASSES classes, the last
-// holding the rest).  Each class keeps queue order (a stable counting sort), so consecutive tiles of
-// one class stay spatially coherent -- which a full longest-first sort loses -- and
-// the cheapest tiles are taken last, where they fill the frame's tail (§10l: 6 classes against the
-// round-3 two, lucy 1080p +3.7 %, bunny +0.5 %).
+// then orders the queue by cost class: the tiles whose cost estimate exceeds `factor` x the mean
+// first, then those above factor r, factor r^2, ... x the mean (SP_TILE_CLASSES classes, ratio r =
+// SP_TILE_RATIO, the last holding the rest).  Each class keeps queue order (a stable counting sort),
+// so consecutive tiles of one class stay spatially coherent -- which a full longest-first sort loses
+//  -- and the cheapest tiles are taken last, where they fill the frame's tail.
+// Round 4 (§10l): 6 classes an octave apart.  Round 5 (§11l): replaying the measured bunny timeline
+// as list scheduling showed that the octave-wide classes themselves left the tail (a 30 ms tile of
+// the 15-31 ms class taken at 230 ms; tools/tile_sched_sim.py): 24 classes a quarter octave apart
+// measured bunny +0.3 %, lucy +1.6 %, elf's 8-way shard +3.5 %.
 // Only which wave takes which tile, and when, changes: every pixel's result is the same.
 #ifndef SP_TILE_CLASSES
-#define SP_TILE_CLASSES 6
+#define SP_TILE_CLASSES 24
 #endif
 constexpr int TILE_CLASSES = SP_TILE_CLASSES;
+#ifndef SP_TILE_RATIO
+#define SP_TILE_RATIO 0.84089642f // 2^(-1/4)
+#endif
 __device__ __forceinline__ int tile_class(float t, float thr)
 {
     int k = 0;
 #pragma unroll
-    for (int j = 0; j + 1 < TILE_CLASSES; ++j, thr *= 0.5f) k += t > thr ? 0 : 1;
-    return k; // 0: slower than thr; class j + 1: not slower than thr / 2^j
+    for (int j = 0; j + 1 < TILE_CLASSES; ++j, thr *= SP_TILE_RATIO) k += t > thr ? 0 : 1;
+    return k; // 0: slower than thr; class j + 1: not slower than thr r^j
 }
 #ifndef SP_TILE_SMOOTH
 #define SP_TILE_SMOOTH 1
 #endif
-// a tile's cost estimate: its probe time blended with its queue neighbours' (for a whole frame: the
-// tiles left and right of it; smooth = false for a caller's tile list, whose queue neighbours need
-// not be image neighbours), against the one-sample probe's noise (profiles/r04/tile_classes/
-// ab_smooth.txt: bunny +0.3-0.5 %, lucy +0.6 %, elf's 8-way shard level; SP_TILE_SMOOTH 0: the probe
-// time alone)
-__device__ __forceinline__ float tile_est(const float* t, int64_t i, int64_t n, bool smooth)
+// A tile's cost estimate: its one-sample probe time blended with its image neighbours', against
+// the probe's noise -- the larger of the row blend (left, right) and the column blend (above,
+// below), so a tile next to an expensive region is not taken late.  tx: the queue offset of the
+// tile below (> 0), -1 when only left / right are image neighbours, 0 when no queue neighbour is
+// (a caller's list in arbitrary order: the probe time alone); sp_capi.hip order_neighbours.
+// Measured against the row blend alone (round 4's form) and the probe time alone: lucy +0.9-1.5 %,
+// elf's 8-way shard +1.3 %, bunny level (profiles/r05/tile_order/).  SP_TILE_SMOOTH 0: probe time alone.
+__device__ __forceinline__ float tile_est(const float* t, int64_t i, int64_t n, int tx)
 {
-    if (!SP_TILE_SMOOTH || !smooth) return t[i];
+    if (!SP_TILE_SMOOTH || tx == 0) return t[i];
     const float l = t[i > 0 ? i - 1 : i], r = t[i + 1 < n ? i + 1 : i];
-    return 0.25f * (l + r) + 0.5f * t[i];
+    const float row = 0.25f * (l + r) + 0.5f * t[i];
+    if (tx < 0) return row;
+    const float u = t[i >= tx ? i - tx : i], d = t[i + tx < n ? i + tx : i];
+    return fmaxf(row, 0.25f * (u + d) + 0.5f * t[i]);
 }
-__global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time, int64_t n, float factor, bool smooth, int32_t* order)
+__global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time, int64_t n, float factor, int tx, int32_t* order)
 {
     __shared__ float s_sum[16];
     __shared__ int   s_cnt[TILE_CLASSES][16];
@@ -94,26 +105,24 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time
     float total = 0.0f;
     for (int w = 0; w < 16; ++w) total += s_sum[w];
     const float thr = factor * total / (float)n;
-    // class sizes -> each class's first position (classes in order 0, 1, ...)
-    for (int k = 0; k < TILE_CLASSES; ++k) {
-        int cnt = 0;
-        for (int64_t i = tid; i < n; i += 1024) cnt += tile_class(tile_est(tile_time, i, n, smooth), thr) == k ? 1 : 0;
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-        if (lane == 0) s_cnt[k][wave] = cnt;
-    }
+    // class sizes (one pass, LDS histogram) -> each class's first position (classes in order 0, 1, ...)
+    __shared__ int s_hist[TILE_CLASSES];
+    for (int k = tid; k < TILE_CLASSES; k += 1024) s_hist[k] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += 1024) atomicAdd(&s_hist[tile_class(tile_est(tile_time, i, n, tx), thr)], 1);
     __syncthreads();
     if (tid == 0) {
         int b = 0;
         for (int k = 0; k < TILE_CLASSES; ++k) {
             s_base[k] = b;
-            for (int w = 0; w < 16; ++w) b += s_cnt[k][w];
+            b += s_hist[k];
         }
     }
     __syncthreads();
     for (int64_t c0 = 0; c0 < n; c0 += 1024) {
         const int64_t i   = c0 + tid;
         const bool    v   = i < n;
-        const int     cls = v ? tile_class(tile_est(tile_time, i, n, smooth), thr) : -1;
+        const int     cls = v ? tile_class(tile_est(tile_time, i, n, tx), thr) : -1;
         uint32_t      pos = 0;
         for (int k = 0; k < TILE_CLASSES; ++k) {
             const uint64_t  m = __ballot(cls == k);
@@ -135,10 +144,10 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time
     }
 }
 
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, bool smooth, int32_t* order,
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
                              hipStream_t stream)
 {
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_time, n_tiles, factor, smooth, order);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_time, n_tiles, factor, tiles_x, order);
     return hipGetLastError();
 }
 

@@ -165,7 +165,7 @@ KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 KernelFn probe_direct(int variant); // nullptr: no probe kernel (queue order)
 KernelFn probe_rrnee(int waves);
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, bool smooth, int32_t* order,
+hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
                              hipStream_t stream);
 
 } // namespace spd
