@@ -164,6 +164,21 @@ def test_tile_order_probe_is_invisible(scene_dir, integrator):
         assert np.array_equal(sub.view(np.uint32), ref[ids].view(np.uint32)), factor
 
 
+@pytest.mark.parametrize("integrator", ["direct_lighting", "iterative_rrnee"])
+def test_tile_order_on_strided_lists(scene_dir, integrator):
+    # a host list in image order with a constant stride (a rank's interleaved shard) gets the
+    # neighbour-blended estimate (sp_capi.hip order_neighbours: the tile below when the stride
+    # divides tiles_x, else left / right only); the list as a whole frame (stride 1), a stride that
+    # divides the 160 tiles per row (2, 4) and one that does not (3) all render the frame's rows
+    s = load(scene_dir, "bunny.sp", 1280, 1024)  # 20480 tiles, 160 per row
+    ref, _ = sp.render_tiles(s, integrator, 2, pipeline="megakernel", tile_order_factor=-1.0)
+    for k in (1, 2, 3, 4):
+        ids = np.arange(k - 1, ref.shape[0], k, dtype=np.int32)
+        sub, st = sp.render_tiles(s, integrator, 2, ids, pipeline="megakernel", tile_order_factor=2.0)
+        assert st.launches == 3, k  # the order ran: more tiles than persistent waves
+        assert np.array_equal(sub.view(np.uint32), ref[ids].view(np.uint32)), k
+
+
 @pytest.mark.parametrize("pipeline", ["megakernel", "chunks", "wavefront"])
 def test_device_ids_outside_the_image_render_zeros(scene_dir, pipeline):
     # a device tile list is not checked on the host: ids outside [0, tiles) -- negative ones too --
