@@ -211,7 +211,7 @@ typedef struct sp_render_params {
     float          tile_order_factor; /* megakernel tile order (DirectLighting, IterativeRRNEE): 0 =
                                          automatic (a one-sample probe times every tile; tiles
                                          slower than 2x the mean go first, then 24 cost classes a
-                                         quarter octave apart; from 4 tiles per wave and 64 spp,
+                                         quarter octave apart; from 6 tiles per wave and 128 spp,
                                          IterativeRRNEE from 4 tiles per wave and 16 spp);
                                          > 0: with this factor whenever it can apply; < 0: queue
                                          order.  It cannot apply, and the frame renders in queue

@@ -1346,15 +1346,14 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // so the frame does not end with a few waves finishing expensive tiles alone.  Part of the
         // render (timed with it); stream-ordered, no host wait.  Used where it measured faster
         // (profiles/r03/ab_tile_order.txt, profiles/r04/tile_classes/): DirectLighting with many
-        // tiles per persistent wave and a probe that costs little of the frame: from 4 tiles per wave
-        // and 64 spp (bunny 1080p @ 256 spp, 7.9 tiles per wave; lucy; spheres 1024^2 @ 64 spp, 4
-        // tiles per wave, lost 1 % with 6 classes, +0.7 % with 24: profiles/r05/tile_order/ab_auto.txt);
+        // tiles per persistent wave and a probe that costs little of the frame (bunny 1080p @ 256
+        // spp, 7.9 tiles per wave; lucy; spheres 1024^2 @ 64 spp, 4 tiles per wave, loses 1 %);
         // IterativeRRNEE, whose tile costs spread wider (paths end at any depth), from 4 tiles per
         // wave and 16 spp (elf 1024^2 @ 16 spp +1.7 %; elf's 8-way shard +3 % with two classes, +5 % more with six).  DirectLighting and
         // IterativeRRNEE have probe kernels (sp_probe_*.hip); the other integrators render in queue
         // order.  sp_render_params.tile_order_factor > 0 forces it with that factor, < 0 turns it off.
         const bool rrnee = integ == SP_INTEGRATOR_ITERATIVE_RRNEE;
-        float      hoist = (n_tiles >= 4 * (int64_t)waves && p->samples_per_pixel >= (rrnee ? 16u : 64u)) ? 2.0f : 0.0f;
+        float      hoist = (n_tiles >= (rrnee ? 4 : 6) * (int64_t)waves && p->samples_per_pixel >= (rrnee ? 16u : 128u)) ? 2.0f : 0.0f;
         if (p->tile_order_factor != 0.0f) hoist = std::max(0.0f, p->tile_order_factor);
         if (hoist > 0.0f && n_tiles > (int64_t)waves && spd::has_probe(integ)) {
             if ((size_t)n_tiles > s->order_cap) {

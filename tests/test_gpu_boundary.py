@@ -150,7 +150,7 @@ def test_tile_order_probe_is_invisible(scene_dir, integrator):
     # which wave renders which tile and when: images and ray / draw counts equal queue order's,
     # also for a tile subset in a shuffled order
     s = load(scene_dir, "bunny.sp", 640, 512)  # 5120 tiles: more than the persistent waves (4096)
-    # forced (tile_order_factor): AUTO uses it from 4 tiles per wave and 64 spp (IterativeRRNEE: 4, 16)
+    # forced (tile_order_factor): AUTO uses it from 6 tiles per wave and 128 spp (IterativeRRNEE: 4, 16)
     ref, rst = sp.render_tiles(s, integrator, 2, pipeline="megakernel", tile_order_factor=2.0)
     # probe, partition, render; integrators without a probe kernel (sp_probe_*.hip) keep queue order
     assert rst.launches == (1 if integrator == "whitted" else 3)
