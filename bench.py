@@ -89,14 +89,20 @@ def parse():
     ap.add_argument("--per-lane-queries", action="store_true",
                     help="IterativeRRNEE: walk every ray on its own lane (SP_RENDER_PER_LANE_QUERIES; comparison)")
     ap.add_argument("--sim-world", type=int, default=0,
-                    help="diagnostic: render only rank 0's shard of an N-GPU run on this one GPU (per-GPU load at N)")
+                    help="diagnostic: render only one rank's shard of an N-GPU run on this one GPU (per-GPU load at N)")
+    ap.add_argument("--sim-rank", type=int, default=0,
+                    help="with --sim-world N: the rank whose shard is rendered (0..N-1); -1 = every rank's shard in "
+                         "turn, one diagnostic JSON line with per-rank times and max/mean (no CPU baseline)")
     ap.add_argument("--traffic-json", default=None,
                     help="tools/pmc_traffic.py output of this workload (default profiles/pmc_bench_<scene>[_shard<N>].json)")
     ap.add_argument("--valu-json", default=None,
                     help="tools/pmc_valu.py output of a PMC pass of this workload (VALU-issue roofline; default "
                          "profiles/pmc_valu_bench_<scene>[_shard<N>].json)")
     a = ap.parse_args()
-    tag = a.scene + (f"_shard{a.sim_world}" if a.sim_world > 1 else "")  # tools/gpu_pmc_*.sh output names
+    if a.sim_world > 1 and not -1 <= a.sim_rank < a.sim_world:
+        ap.error("--sim-rank must be -1 or in [0, --sim-world)")
+    # tools/gpu_pmc_*.sh output names (PMC passes profile rank 0's shard)
+    tag = a.scene + (f"_shard{a.sim_world}" if a.sim_world > 1 else "") + (f"_r{a.sim_rank}" if a.sim_world > 1 and a.sim_rank > 0 else "")
     a.traffic_json = a.traffic_json or os.path.join(ROOT, "profiles", f"pmc_bench_{tag}.json")
     a.valu_json = a.valu_json or os.path.join(ROOT, "profiles", f"pmc_valu_bench_{tag}.json")
     sc = SCENES[a.scene]
@@ -231,7 +237,9 @@ def main():
     my_tiles = shard.shard_tiles(n_tiles, rank, world)
     per_rank = shard.per_rank_capacity(n_tiles, world)
     if args.sim_world > 1 and world == 1:
-        my_tiles = shard.shard_tiles(n_tiles, 0, args.sim_world)
+        if args.sim_rank < 0:
+            return sim_all_ranks(args, scene, integ, n_tiles, rdev)
+        my_tiles = shard.shard_tiles(n_tiles, args.sim_rank, args.sim_world)
         per_rank = shard.per_rank_capacity(n_tiles, args.sim_world)
     out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=rdev)
     gathered, frame = None, None
@@ -388,6 +396,53 @@ def main():
             line["test_post_stall_s"] = stall
     print(json.dumps(line), flush=True)
     os.dup2(2, 1)  # exit-time log summaries of the reference library go to stderr
+
+
+def sim_all_ranks(args, scene, integ, n_tiles, rdev):
+    """--sim-world N --sim-rank -1: every rank's shard of an N-rank frame rendered on this one GPU in
+    turn (warm-up, then --steps timed frames each; the same tiles and calls a rank makes, no
+    collective), so the per-rank balance of the partition can be measured without N GPUs.  Prints
+    one diagnostic line: per-rank ms per frame, render-kernel ms, rays; max / mean of each."""
+    import torch
+
+    import simplepath_amd as sp
+    from simplepath_amd import shard
+
+    stream = torch.cuda.current_stream().cuda_stream
+    per_rank = shard.per_rank_capacity(n_tiles, args.sim_world)
+    out = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=rdev)
+    ranks = []
+    for r in range(args.sim_world):
+        tiles = shard.shard_tiles(n_tiles, r, args.sim_world)
+
+        def render():
+            return sp.render_tiles_device(scene, integ, args.spp, tiles, out.data_ptr(), stream, pipeline=args.pipeline,
+                                          stage_timing=True, waves_per_simd=args.waves,
+                                          tile_order_factor=args.tile_order_factor)
+        for _ in range(args.warmup):
+            render()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = [render() for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        rays = sum(x.rays for x in st) / args.steps
+        ranks.append({"rank": r, "tiles": int(len(tiles)), "ms_per_frame": round(ms, 3),
+                      "kernel_ms": round(sum(x.kernel_ms for x in st) / args.steps, 3),
+                      "rays": int(rays), "mrays_per_s": round(rays / ms / 1e3, 2),
+                      "pipeline": ["auto", "megakernel", "wavefront", "chunks"][st[-1].pipeline]})
+        print(json.dumps(ranks[-1]), file=sys.stderr, flush=True)
+
+    def imb(key):
+        v = [x[key] for x in ranks]
+        return round(max(v) / (sum(v) / len(v)), 4)
+    line = {"diag": "sim_ranks", "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+            "integrator": args.integrator, "sim_world": args.sim_world, "shard": "interleaved (shard.shard_tiles)",
+            "steps": args.steps, "warmup": args.warmup, "ranks": ranks,
+            "imbalance_ms": imb("ms_per_frame"), "imbalance_rays": imb("rays"),
+            "frame_ms_at_n": max(x["ms_per_frame"] for x in ranks),
+            "library": sp._abi.build_identity()}
+    print(json.dumps(line), flush=True)
 
 
 def stage_bytes(st, pixels):

@@ -220,9 +220,11 @@ typedef struct sp_render_params {
                                          the persistent waves (each wave takes one tile), or for
                                          an integrator without a probe kernel (BruteForce*,
                                          Whitted, Mandelbrot).  A tile's estimate is its probe time
-                                         blended with its image neighbours' for a whole frame or a
-                                         host list in image order with a constant stride (a rank's
-                                         interleaved shard); any other list uses each tile's own
+                                         blended with its queue neighbours' for a whole frame (the
+                                         tiles left, right, above and below) or a host list with a
+                                         constant stride k (a rank's interleaved shard: the tiles k
+                                         columns left and right, and the tile below when k divides
+                                         the tile columns); any other list uses each tile's own
                                          probe time.                                                  */
     int32_t        reserved[2];       /* must be 0                                                  */
 } sp_render_params;

@@ -94,6 +94,9 @@ SP_HD float x86_add(float a, float b)
 // ------------------------------------------------------------------------------------ expf
 SP_HD float lm_expf(float x)
 {
+#if defined(SP_XP_FASTLIBM) && defined(__HIP_DEVICE_COMPILE__) // timing-only bound (sp_path.hpp SP_XP_*)
+    return __expf(x);
+#endif
     using namespace glibc;
     const uint32_t ix     = f2u(x);
     const uint32_t abstop = (ix >> 20) & 0x7ffu;
@@ -123,6 +126,9 @@ SP_HD float lm_expf(float x)
 // ------------------------------------------------------------------------------------ logf
 SP_HD float lm_logf(float x)
 {
+#if defined(SP_XP_FASTLIBM) && defined(__HIP_DEVICE_COMPILE__) // timing-only bound (sp_path.hpp SP_XP_*)
+    return __logf(x);
+#endif
     using namespace glibc;
     uint32_t ix = f2u(x);
     if (ix == 0x3f800000u) return 0.0f;
@@ -163,6 +169,9 @@ SP_HD bool issignalingf(uint32_t ix) { return ((ix & 0x7fffffffu) > 0x7f800000u)
 
 SP_HD float lm_powf(float x, float y)
 {
+#if defined(SP_XP_FASTLIBM) && defined(__HIP_DEVICE_COMPILE__) // timing-only bound (sp_path.hpp SP_XP_*)
+    return __powf(x, y);
+#endif
     using namespace glibc;
     uint32_t       sign_bias = 0;
     uint32_t       ix = f2u(x);
@@ -291,6 +300,9 @@ SP_HD double sincosf_reduce_large(uint32_t xi, int* np)
 template <bool BOUNDED = false>
 SP_HD float lm_sinf(float y)
 {
+#if defined(SP_XP_FASTLIBM) && defined(__HIP_DEVICE_COMPILE__) // timing-only bound (sp_path.hpp SP_XP_*)
+    return __sinf(y);
+#endif
     const uint32_t iy     = f2u(y);
     const uint32_t abstop = (iy >> 20) & 0x7ffu;
     double         x      = (double)y;
@@ -322,6 +334,9 @@ SP_HD float lm_sinf(float y)
 template <bool BOUNDED = false> // as lm_sinf
 SP_HD float lm_cosf(float y)
 {
+#if defined(SP_XP_FASTLIBM) && defined(__HIP_DEVICE_COMPILE__) // timing-only bound (sp_path.hpp SP_XP_*)
+    return __cosf(y);
+#endif
     const uint32_t iy     = f2u(y);
     const uint32_t abstop = (iy >> 20) & 0x7ffu;
     double         x      = (double)y;

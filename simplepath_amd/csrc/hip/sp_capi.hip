@@ -974,7 +974,17 @@ static ChunkPlan chunk_plan(const sp_scene* s, int64_t n_tiles, uint32_t spp, in
 }
 
 // Queue neighbours of the tile-order kernel's cost estimate (sp_mega.hip tile_est): > 0 the queue
-// offset of the tile below (left / right at +-1), -1 left / right only, 0 none.
+// offset of the tile below, -1 the +-1 queue neighbours only, 0 none.  The tile ids are row-major
+// (base/TileScheduler.h:75-77: x = index % tiles_x), so for a whole frame (k = 1) the +-1 queue
+// neighbours are the tiles left and right.  For a host list with a constant stride k > 1 (a rank's
+// interleaved shard) they are the tiles k columns to the left and right -- the same row, not
+// adjacent -- and the tile below is tiles_x / k entries on when k divides tiles_x; otherwise
+// (-1) the rows of consecutive entries shift and only the +-1 entries are used.  SP_TILE_STRIDE_ROW
+// 0 drops the +-1 entries for k > 1 (the column blend alone, or the probe time alone when k does
+// not divide tiles_x).  Row blend kept for k > 1 by an A/B on elf's 8-way shard.
+#ifndef SP_TILE_STRIDE_ROW
+#define SP_TILE_STRIDE_ROW 1
+#endif
 static int order_neighbours(const sp_render_params* p, bool listed, int64_t n_tiles, int32_t tiles_x)
 {
     if (!listed) return tiles_x;
@@ -983,6 +993,7 @@ static int order_neighbours(const sp_render_params* p, bool listed, int64_t n_ti
     if (k <= 0) return 0;
     for (int64_t i = 2; i < n_tiles; ++i)
         if ((int64_t)p->tile_ids[i] - p->tile_ids[i - 1] != k) return 0;
+    if (k > 1 && !SP_TILE_STRIDE_ROW) return (tiles_x % k == 0) ? -(int)(tiles_x / k) - 1 : 0;
     return (tiles_x % k == 0) ? (int)(tiles_x / k) : -1;
 }
 
@@ -1335,8 +1346,10 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         const char*         tdiag_path = std::getenv("SP_TILE_DIAG");
         unsigned long long* tdiag      = nullptr;
         if (tdiag_path) {
-            SP_HIP(hipMalloc(&tdiag, (size_t)n_tiles * 8 * sizeof(unsigned long long)));
-            SP_HIP(hipMemsetAsync(tdiag, 0, (size_t)n_tiles * 8 * sizeof(unsigned long long), stream));
+            // the -DSP_WAVE_PROF / -DSP_TRAFFIC_DIAG builds add their totals into words 0..47
+            const size_t words = std::max<size_t>((size_t)n_tiles * 8, 48);
+            SP_HIP(hipMalloc(&tdiag, words * sizeof(unsigned long long)));
+            SP_HIP(hipMemsetAsync(tdiag, 0, words * sizeof(unsigned long long), stream));
         }
         a.tile_diag = tdiag;
         a.order     = nullptr;
@@ -1373,9 +1386,9 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
             SP_HIP(spd::launch_probe(sc_run, pr, integ, variant, blocks, lds_bytes, stream));
-            // cost estimates blended with their queue neighbours only where those are image
-            // neighbours: a whole frame, or a host list in image order with a constant stride (the
-            // bench's list, a rank's interleaved shard); any other list keeps each tile's own time
+            // cost estimates blended with their queue neighbours only where those sit at known
+            // image offsets: a whole frame, or a host list with a constant stride (the bench's list,
+            // a rank's interleaved shard; order_neighbours); any other list keeps each tile's own time
             SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, order_neighbours(p, listed, n_tiles, a.tiles_x),
                                           s->d_order, stream));
             SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));

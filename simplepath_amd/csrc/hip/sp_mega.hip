@@ -56,7 +56,8 @@ hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int 
 // Round 4 (§10l): 6 classes an octave apart.  Round 5 (§11l): replaying the measured bunny timeline
 // as list scheduling showed that the octave-wide classes themselves left the tail (a 30 ms tile of
 // the 15-31 ms class taken at 230 ms; tools/tile_sched_sim.py): 24 classes a quarter octave apart
-// measured bunny +0.3 %, lucy +1.6 %, elf's 8-way shard +3.5 %.
+// measured bunny +0.3 %, lucy +1.6 %, elf's 8-way shard +1.6-3.5 % (elf: single-frame runs, --steps 1
+// --warmup 0; re-measured with warm-up and 2 steps in DESIGN.md §12).
 // Only which wave takes which tile, and when, changes: every pixel's result is the same.
 #ifndef SP_TILE_CLASSES
 #define SP_TILE_CLASSES 24
@@ -78,13 +79,20 @@ __device__ __forceinline__ int tile_class(float t, float thr)
 // A tile's cost estimate: its one-sample probe time blended with its image neighbours', against
 // the probe's noise -- the larger of the row blend (left, right) and the column blend (above,
 // below), so a tile next to an expensive region is not taken late.  tx: the queue offset of the
-// tile below (> 0), -1 when only left / right are image neighbours, 0 when no queue neighbour is
-// (a caller's list in arbitrary order: the probe time alone); sp_capi.hip order_neighbours.
+// tile below (> 0), -1 when only the +-1 queue entries are used, < -1 the column blend alone with
+// offset -tx - 1, 0 none (a caller's list in arbitrary order: the probe time alone); the +-1 entries
+// are the left / right tiles of a whole frame and k tiles apart in a stride-k list
+// (sp_capi.hip order_neighbours).
 // Measured against the row blend alone (round 4's form) and the probe time alone: lucy +0.9-1.5 %,
 // elf's 8-way shard +1.3 %, bunny level (profiles/r05/tile_order/).  SP_TILE_SMOOTH 0: probe time alone.
 __device__ __forceinline__ float tile_est(const float* t, int64_t i, int64_t n, int tx)
 {
     if (!SP_TILE_SMOOTH || tx == 0) return t[i];
+    if (tx < -1) {
+        const int64_t o = -(int64_t)tx - 1;
+        const float   u = t[i >= o ? i - o : i], d = t[i + o < n ? i + o : i];
+        return 0.25f * (u + d) + 0.5f * t[i];
+    }
     const float l = t[i > 0 ? i - 1 : i], r = t[i + 1 < n ? i + 1 : i];
     const float row = 0.25f * (l + r) + 0.5f * t[i];
     if (tx < 0) return row;

@@ -156,6 +156,9 @@ __device__ __forceinline__ float sqrt_unit(float x)
 #ifndef SP_RNG_PF
 #define SP_RNG_PF 2
 #endif
+#ifndef SP_XP_SERVED_FREE
+#define SP_XP_SERVED_FREE 0
+#endif // timing-only bound (SP_XP_* below)
 constexpr int RNG_PF = SP_RNG_PF;
 struct Rng {
     uint64_t* base;  // this lane's base in its wave slot's state (sp_device.hpp mt_off layout)
@@ -393,6 +396,8 @@ __device__ __forceinline__ uint64_t rng_raw(Rng& r)
 #pragma unroll
         for (int k = 0; k + 1 < RNG_PF; ++k) r.pf[k] = r.pf[k + 1];
         --r.pfn;
+    } else if (SP_XP_SERVED_FREE && r.lin == 2) { // timing-only bound: hashed words, no read
+        w = ((uint64_t)(r.idx + 1000 * r.cur + 7) * 0x9E3779B97F4A7C15ull) ^ (uint64_t)(uintptr_t)r.base;
     } else {
         SP_TD(td_lines(r.td_cat, &b[mt_off(r.idx)], 8));
         w = b[mt_off(r.idx)];
@@ -457,6 +462,7 @@ __device__ __forceinline__ void rng_skip_reserved(Rng& r, int n)
 // touched in the next buffer only when it already holds the next generation.
 __device__ __forceinline__ void rng_touch(const Rng& r, int n, __attribute__((address_space(3))) void* sink)
 {
+    if (SP_XP_SERVED_FREE && r.lin == 2) return;
     const uint64_t* cur  = r.base + (size_t)r.cur * MT_GEN_WORDS;
     const uint64_t* next = r.base + (size_t)mt_next(r) * MT_GEN_WORDS;
     if constexpr (MT_BLK == 1) {
@@ -520,7 +526,10 @@ static __shared__ uint32_t rho_rng_sink[64];
 template <bool NT = false>
 __device__ __forceinline__ void rng_raw2(Rng& r, uint64_t& w0, uint64_t& w1)
 {
-    if constexpr (SP_RNG_PAIR && MT_BLK >= 2 && RNG_PF == 0) {
+    // pairs need even lane blocks: with MT_BLK % 2 != 0 (e.g. 3) words 2j, 2j + 1 can sit in two
+    // blocks and a lane's block is not 16-byte aligned
+    static_assert(!SP_RNG_PAIR || MT_BLK == 1 || MT_BLK % 2 == 0, "SP_RNG_PAIR needs an even MT_BLK");
+    if constexpr (SP_RNG_PAIR && MT_BLK >= 2 && MT_BLK % 2 == 0 && RNG_PF == 0) {
         if (r.idx >= MT_N) { // the buffer switch of rng_raw
             if (!NT && !r.ready) {
                 SP_TD(td_twist(TD_TWIST));
@@ -712,6 +721,54 @@ __device__ __forceinline__ Isect finish_hit(const Scene& sc, const Hit& h, const
     return is;
 }
 
+// ---------------------------------------------------------------- timing-only bounds (SP_XP_*)
+// Experiment builds only (wrong or unchanged images, never the product): each measures how much a
+// cost could matter before anything is built against it.
+//   SP_XP_DUP 1: every 8-wide node fetch is issued twice (the second through an address the
+//     compiler cannot prove equal, its words OR-ed in under a zero mask): twice the vector-L1
+//     lookups of node fetches, same walk and same image -- the sensitivity of the frame to them;
+//     2: the wide-leaf triangle records too.
+//   SP_XP_FASTLIBM: expf / logf / powf / sinf / cosf as the native f32 instructions (wrong image):
+//     the upper bound of replacing the exact glibc emulation's f64 arithmetic.
+//   SP_XP_SERVED_FREE: served estimates (IterativeRRNEE) draw hashed words instead of reading the
+//     owner's stream (wrong image): the upper bound of making their reads free.
+#ifndef SP_XP_DUP
+#define SP_XP_DUP 0
+#endif
+#if SP_XP_DUP
+__device__ __forceinline__ uint32_t xp_zero()
+{
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+__device__ __forceinline__ void xp_or(uint4& w, const uint4& d, uint32_t z)
+{
+    w.x |= d.x & z; w.y |= d.y & z; w.z |= d.z & z; w.w |= d.w & z;
+}
+__device__ __forceinline__ void xp_dup(const uint4* p, uint4& w0, uint4& w1, uint4& w2, uint4& w3, uint4& w4)
+{
+    const uint32_t z = xp_zero();
+    const uint4*   q = p + z;
+    const uint4    d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+    xp_or(w0, d0, z); xp_or(w1, d1, z); xp_or(w2, d2, z); xp_or(w3, d3, z); xp_or(w4, d4, z);
+}
+__device__ __forceinline__ void xp_orf(float4& w, const float4& d, uint32_t z)
+{
+    w.x = __uint_as_float(__float_as_uint(w.x) | (__float_as_uint(d.x) & z));
+    w.y = __uint_as_float(__float_as_uint(w.y) | (__float_as_uint(d.y) & z));
+    w.z = __uint_as_float(__float_as_uint(w.z) | (__float_as_uint(d.z) & z));
+    w.w = __uint_as_float(__float_as_uint(w.w) | (__float_as_uint(d.w) & z));
+}
+__device__ __forceinline__ void xp_dup3(const float4* p, float4& q0, float4& q1, float4& q2)
+{
+    const uint32_t z = xp_zero();
+    const float4*  q = p + z;
+    const float4   d0 = q[0], d1 = q[1], d2 = q[2];
+    xp_orf(q0, d0, z); xp_orf(q1, d1, z); xp_orf(q2, d2, z);
+}
+#endif
+
 // Test one primitive code against the ray (closest-hit semantics: t <= tmax accepted).
 __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h,
                                              const float4* tris = nullptr)
@@ -745,8 +802,13 @@ __device__ __forceinline__ bool prim_closest(const Scene& sc, uint32_t slot, con
 __device__ __forceinline__ bool prim_closest_w(const Scene& sc, uint32_t slot, const Ray& ray, float tmin, Hit& h)
 {
     SP_TD(td_lines(TD_TRI, &sc.wslot_tri[3 * slot], 48));
+#if SP_XP_DUP >= 2
+    float4 q0 = sc.wslot_tri[3 * slot], q1 = sc.wslot_tri[3 * slot + 1], q2 = sc.wslot_tri[3 * slot + 2];
+    xp_dup3(&sc.wslot_tri[3 * slot], q0, q1, q2);
+#else
     const float4   q0   = sc.wslot_tri[3 * slot]; // p0 | code
     const float4   q1 = sc.wslot_tri[3 * slot + 1], q2 = sc.wslot_tri[3 * slot + 2]; // issued with q0
+#endif
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     float          t, be = 0.0f, ga = 0.0f;
@@ -767,8 +829,13 @@ __device__ __forceinline__ bool prim_any(const Scene& sc, uint32_t slot, const R
 {
     const float4*  st   = tris ? tris : sc.slot_tri;
     SP_TD(td_lines(tris ? TD_TRI : TD_BIN, &st[3 * slot], 48));
+#if SP_XP_DUP >= 2
+    float4 q0 = st[3 * slot], q1 = st[3 * slot + 1], q2 = st[3 * slot + 2];
+    xp_dup3(&st[3 * slot], q0, q1, q2);
+#else
     const float4   q0   = st[3 * slot]; // p0 | code
     const float4   q1 = st[3 * slot + 1], q2 = st[3 * slot + 2]; // issued with q0
+#endif
     const uint32_t code = __float_as_uint(q0.w);
     const uint32_t kind = code >> CODE_SHIFT;
     if (kind == KIND_TRI) {
@@ -914,7 +981,12 @@ __device__ __forceinline__ WideHits wide_visit(const Scene& sc, uint32_t node, c
 {
     const uint4*   np = sc.wnodes + 5 * (size_t)node;
     SP_TD(td_lines(TD_NODE, np, 80));
+#if SP_XP_DUP >= 1
+    uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+    xp_dup(np, w0, w1, w2, w3, w4);
+#else
     const uint4    w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+#endif
     const float    px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
     const float    sx = __uint_as_float((w0.w & 0xffu) << 23);
     const float    sy = __uint_as_float(((w0.w >> 8) & 0xffu) << 23);
@@ -954,7 +1026,13 @@ __device__ __forceinline__ uint32_t key_mask(uint32_t m, uint32_t o);
 // occ (walk cache, SP_OCC_CACHE): the wide slot of the primitive that occluded this lane's previous
 // shadow ray.  It is tested first; if it occludes this ray too, the answer (an OR over every
 // primitive the ray meets in [tmin, tmax]) is true without a walk.  A hit found by the walk
-// becomes the new cached occluder.  Same answer either way: only which primitives are tested changes.
+// becomes the new cached occluder.  Same answer either way: only which primitives are tested changes
+// -- PROVIDED the walk would have reached the cached primitive, i.e. no box on the way to its leaf
+// is rejected by wbox for a ray that tri_hit accepts in [tmin, tmax].  The quantised boxes are
+// rounded outward (supersets), but the slab t and the Moller-Trumbore t round differently, so for a
+// primitive lying in a box face, hit at t within an ulp or so of tmax, the walk can miss what the
+// cache finds.  The cache relies on that edge case not arising; it is off by default since round 6
+// (level on every DirectLighting config, profiles/r05/walk_cache/), so the default walk is exact.
 __device__ __forceinline__ bool wide_any(const Scene& sc, const Ray& ray, float tmin, float tmax, Stack st,
                                          uint32_t* occ = nullptr)
 {
@@ -2465,8 +2543,8 @@ __device__ __forceinline__ float light_pdf(const Scene& sc, const Light& l, f3 o
 }
 
 // ============================================================================ integrators
-#ifndef SP_OCC_CACHE
-#define SP_OCC_CACHE 1
+#ifndef SP_OCC_CACHE // round 5 default 1; level on every config (profiles/r05/walk_cache/), off since round 6 (wide_any)
+#define SP_OCC_CACHE 0
 #endif
 struct Ctx {
     const Scene& sc;
@@ -2777,6 +2855,7 @@ __device__ __forceinline__ void served_weights(const Material& m, f3 wo, uint64_
     sr.idx   = idx;
     sr.ready = 1;
     sr.draws = 0;
+    if (SP_XP_SERVED_FREE) sr.lin = 2;
     glossy_weights(m, wo, sr, q, w);
 }
 // want: this lane's eval / pdf / sample estimates of the light being estimated (k = 0, 1, 2);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library builds and environment settings on one box, bench.py --no-cpu in alternation.
-#   RUNS       ";"-separated entries "builddir [VAR=value ...]" (default: simplepath_amd/_build_base;
+#   RUNS       ";"-separated entries "builddir [VAR=value ...]" (default: simplepath_amd/_ab/base;
 #              simplepath_amd/_build), repeated REPEAT times (default 2)
 #   WORKLOADS  ";"-separated bench.py argument sets, each run for every entry (default: one set,
 #              BENCH_ARGS).  E.g. WORKLOADS="; --scene elf --width 1024 --height 1024 --spp 16; --sim-world 8"
@@ -14,7 +14,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
-IFS=';' read -ra RN <<< "${RUNS:-simplepath_amd/_build_base;simplepath_amd/_build}"
+IFS=';' read -ra RN <<< "${RUNS:-simplepath_amd/_ab/base;simplepath_amd/_build}"
 IFS=';' read -ra WL <<< "${WORKLOADS:-}"
 [ ${#WL[@]} -eq 0 ] && WL=("")
 if [ -n "${SMOKE:-}" ]; then

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Wave-level region profile (-DSP_WAVE_PROF build in simplepath_amd/_build_wprof, tools/wprof.py).
+# Wave-level region profile (-DSP_WAVE_PROF build in simplepath_amd/_ab/wprof, tools/wprof.py).
 #   WPROF_RUNS  ";"-separated bench.py argument lists (default: elf 1024^2 @ 16 spp; bunny 1080p)
 set -o pipefail
 mkdir -p gpurun_out/wprof
-lib=$PWD/simplepath_amd/_build_wprof/libsimplepath_hip.so
+lib=$PWD/simplepath_amd/_ab/wprof/libsimplepath_hip.so
 IFS=';' read -ra RN <<< "${WPROF_RUNS:---scene elf --width 1024 --height 1024 --spp 16;--spp 64}"
 i=0
 for a in "${RN[@]}"; do
