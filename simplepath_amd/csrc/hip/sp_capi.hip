@@ -26,6 +26,8 @@ hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float fact
 bool       has_probe(int integ);
 hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
                         hipStream_t stream);
+hipError_t launch_tail(const Scene& sc, const RenderArgs& args, int blocks, size_t lds_bytes, hipStream_t stream);
+int        tail_blocks_per_cu(size_t lds_bytes);
 } // namespace spd
 
 namespace {
@@ -239,6 +241,8 @@ struct sp_scene {
     int32_t*             d_order     = nullptr;
     size_t               order_cap   = 0;
     unsigned long long*  probe_counters = nullptr;
+    void*                tail_buf    = nullptr; // megakernel tail chunks: TailArgs, flags, hits, radiance, store
+    size_t               tail_cap    = 0;
     // One scene, many host threads (the reference's render() shares one Scene across N threads,
     // main.cpp:122-130): the render scratch above is per scene, so calls are serialised -- on the
     // host by `mu`, and on the device by making each call's stream wait for the previous call's
@@ -298,6 +302,8 @@ struct sp_scene {
         if (d_order) (void)hipFree(d_order);
         if (probe_counters) (void)hipFree(probe_counters);
         d_tile_time = nullptr; d_order = nullptr; order_cap = 0; probe_counters = nullptr;
+        if (tail_buf) (void)hipFree(tail_buf);
+        tail_buf = nullptr; tail_cap = 0;
         if (ev_done) (void)hipEventDestroy(ev_done);
         ev_done = nullptr; done_rec = false;
         for (int k = 0; k < STAGE_RING; ++k) {
@@ -934,6 +940,15 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
     }
 }
 
+// Megakernel tail chunks (render_tiles_impl): the fraction of the tiles cut into sample chunks at
+// the end of the queue, and chunks per tile.
+#ifndef SP_TAIL_FRAC
+#define SP_TAIL_FRAC 0.0f
+#endif
+#ifndef SP_TAIL_CHUNKS
+#define SP_TAIL_CHUNKS 32
+#endif
+
 // Sample-chunk buffer plan (sp_chunk.hip): the same sizes decide AUTO and are allocated.
 struct ChunkPlan {
     int64_t  chunks = 1;    // chunks per pixel
@@ -1395,11 +1410,74 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             a.order = s->d_order;
             launches += 2;
         }
+        // Tail chunks (sp_mega.hpp, sp_device.hpp TailArgs): the K = tail_frac x n_tiles most
+        // expensive tiles of the order are rendered as sample chunks at the end of the queue.
+        // DirectLighting at 4 waves per SIMD with the tile order and draw counts known from the
+        // camera hits (no image light); SP_TAIL_FRAC (0: off) and SP_TAIL_CHUNKS override.
+        int64_t        tail_k = 0;
+        spd::ChunkArgs tail_sum{};
+        if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && variant == 4 && a.order) {
+            float tail_frac = SP_TAIL_FRAC;
+            int   tail_ch   = SP_TAIL_CHUNKS;
+            if (const char* v = std::getenv("SP_TAIL_FRAC")) tail_frac = (float)std::atof(v);
+            if (const char* v = std::getenv("SP_TAIL_CHUNKS")) tail_ch = std::atoi(v);
+            const ChunkPlan tp = chunk_plan(s, 1, spp_u, std::max(1, tail_ch));
+            if (tail_frac > 0.0f && tp.known_draws) {
+                tail_k = std::min<int64_t>(n_tiles, std::max<int64_t>(1, (int64_t)std::ceil((double)tail_frac * (double)n_tiles)));
+                const ChunkPlan cp    = chunk_plan(s, tail_k, spp_u, std::max(1, tail_ch));
+                const size_t    a_hdr = 256, a_rdy = ((size_t)tail_k * 4 + 255) / 256 * 256;
+                const size_t    need  = a_hdr + a_rdy + cp.b_hits + cp.b_L + cp.b_snap + cp.b_ctl;
+                if (need > s->tail_cap) {
+                    if (s->tail_buf) (void)hipFree(s->tail_buf);
+                    s->tail_buf = nullptr;
+                    s->tail_cap = 0;
+                    SP_HIP(hipMalloc(&s->tail_buf, need));
+                    s->tail_cap = need;
+                }
+                char*         base = static_cast<char*>(s->tail_buf);
+                spd::TailArgs ta{};
+                ta.n_prep      = tail_k;
+                ta.n_items     = tail_k * cp.chunks;
+                ta.chunks      = (uint32_t)cp.chunks;
+                ta.chunk_len   = cp.len;
+                ta.gens_per_px = cp.gens;
+                ta.n_px        = (size_t)tail_k * 64;
+                ta.ready       = reinterpret_cast<uint32_t*>(base + a_hdr);
+                ta.hits        = reinterpret_cast<float4*>(base + a_hdr + a_rdy);
+                ta.L           = reinterpret_cast<float*>(base + a_hdr + a_rdy + cp.b_hits);
+                ta.gens        = reinterpret_cast<uint64_t*>(base + a_hdr + a_rdy + cp.b_hits + cp.b_L);
+                ta.snap_ctl    = reinterpret_cast<uint32_t*>(base + a_hdr + a_rdy + cp.b_hits + cp.b_L + cp.b_snap);
+                // the kernel reads TailArgs from device memory (stream-ordered behind the previous
+                // call's kernels, which may still read it)
+                SP_HIP(hipMemcpyAsync(base, &ta, sizeof(ta), hipMemcpyHostToDevice, stream));
+                SP_HIP(hipMemsetAsync(ta.ready, 0, (size_t)tail_k * 4, stream));
+                a.tail_prep  = ta.n_prep;
+                a.tail_items = ta.n_items;
+                a.tail       = reinterpret_cast<const spd::TailArgs*>(base);
+                tail_sum.tile_ids  = d_ids;
+                tail_sum.num_tiles = tail_k;
+                tail_sum.tiles_x   = a.tiles_x;
+                tail_sum.spp       = spp_u;
+                tail_sum.n_px      = ta.n_px;
+                tail_sum.L         = ta.L;
+                tail_sum.out       = d_out;
+                tail_sum.slot_map  = s->d_order; // chunk slot k is queue item k: tile slot order[k]
+            }
+        }
         if (timing) {
             if (!s->ev_render) SP_HIP(hipEventCreate(&s->ev_render));
             SP_HIP(hipEventRecord(s->ev_render, stream));
         }
-        SP_HIP(spd::launch_render(sc_run, a, integ, variant, blocks, lds_bytes, stream));
+        if (tail_k > 0) {
+            const int     t_per_cu = spd::tail_blocks_per_cu(lds_bytes);
+            const int64_t t_need   = (n_tiles + a.tail_items + 3) / 4;
+            const int     t_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * t_per_cu, t_need));
+            SP_HIP(spd::launch_tail(sc_run, a, t_blocks, lds_bytes, stream));
+            SP_HIP(spd::chunk_sum(sc_run, tail_sum, stream));
+            launches += 1;
+        } else {
+            SP_HIP(spd::launch_render(sc_run, a, integ, variant, blocks, lds_bytes, stream));
+        }
         if (tdiag) { // diagnostic: waits for the render
             SP_HIP(hipStreamSynchronize(stream));
             std::vector<unsigned long long> rec((size_t)n_tiles * 8);

@@ -77,7 +77,8 @@ struct Px {
 };
 __device__ __forceinline__ Px pixel(const Scene& sc, const ChunkArgs& a, int64_t slot, uint32_t lane)
 {
-    const int32_t tile = a.tile_ids ? a.tile_ids[slot] : (int32_t)slot;
+    const int64_t s    = a.slot_map ? (int64_t)a.slot_map[slot] : slot;
+    const int32_t tile = a.tile_ids ? a.tile_ids[s] : (int32_t)s;
     Px            p;
     p.x      = (uint32_t)((tile % a.tiles_x) * 8) + morton_decode_1(lane);
     p.y      = (uint32_t)((tile / a.tiles_x) * 8) + morton_decode_1(lane >> 1);
@@ -111,30 +112,6 @@ __device__ __forceinline__ int64_t grab(int32_t* counter)
     int g = 0;
     if ((threadIdx.x & 63) == 0) g = atomicAdd(counter, 1);
     return __shfl(g, 0, 64);
-}
-
-// Stream words one DirectLighting sample at hit `is` draws (direct_nee, sp_path.hpp): two per
-// light for Light::sample, plus 32 for the glossy rho estimate of Material::eval when the light
-// sample is usable and wo.y != 0 in the shading frame.  For sphere and uniform environment
-// lights usability (pdf != 0, L not black) does not depend on the drawn numbers -- pdf is
-// sphere_pdf(observer) or a constant, L the radiance -- so the count is known from the hit.
-__device__ __forceinline__ uint32_t sample_draws(const Scene& sc, const Isect& is, f3 wo, const Rsq& q)
-{
-    const Material& m    = sc.materials[is.material];
-    const int       base = (m.kind == SP_MAT_CLEARCOAT) ? sc.materials[m.base].kind : m.kind;
-    bool            rho  = false;
-    if (base != SP_MAT_LAMBERTIAN) {
-        const Onb o = onb_from_v(is.n, q);
-        rho         = to_onb(o, wo).y != 0.0f;
-    }
-    uint32_t n = 0;
-    for (int li = 0; li < sc.n_lights; ++li) {
-        const Light lt  = uload_light(sc.lights + li);
-        const float pdf = (lt.kind == SP_LIGHT_SPHERE) ? sphere_pdf(lt, is.p) : k_uniform_sphere_pdf;
-        n += 2;
-        if (rho && !(pdf == 0.0f || cblack(lt.radiance))) n += 32;
-    }
-    return n;
 }
 
 } // namespace
@@ -327,9 +304,10 @@ __global__ void __launch_bounds__(256) ck_sum(Scene sc, ChunkArgs a)
                                 a.L[((size_t)i * 3 + 2) * a.n_px + p])); // image(p) += integrate(...)
         acc = cdivs(acc, (float)a.spp);                                    // image(p) /= num_pixel_samples
     }
-    a.out[(size_t)p * 3 + 0] = acc.r;
-    a.out[(size_t)p * 3 + 1] = acc.g;
-    a.out[(size_t)p * 3 + 2] = acc.b;
+    const int64_t o = (a.slot_map ? (int64_t)a.slot_map[p >> 6] : (p >> 6)) * 64 + (p & 63);
+    a.out[(size_t)o * 3 + 0] = acc.r;
+    a.out[(size_t)o * 3 + 1] = acc.g;
+    a.out[(size_t)o * 3 + 2] = acc.b;
 }
 
 // ck_shade occupancy: 4 waves per SIMD (128 VGPRs, ~116 B spill).  Bunny 8-way shard per GPU:
@@ -365,6 +343,11 @@ hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_bloc
     hipLaunchKernelGGL(shade_kernel(), dim3((unsigned)persistent_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes,
                        stream, sc, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    return chunk_sum(sc, a, stream);
+}
+
+hipError_t chunk_sum(const Scene& sc, const ChunkArgs& a, hipStream_t stream)
+{
     hipLaunchKernelGGL(ck_sum, dim3((unsigned)((a.n_px + 255) / 256)), dim3(256), 0, stream, sc, a);
     return hipGetLastError();
 }

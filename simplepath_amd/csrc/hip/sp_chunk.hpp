@@ -24,9 +24,13 @@ struct ChunkArgs {
     int32_t*            counter;   // [2] work queues of ck_count and ck_shade (zeroed by the caller)
     unsigned long long* counters;  // stats: [1] shadow rays, [3] RNG draws
     float*              out;       // tile-packed radiance [n_px][3]
+    const int32_t*      slot_map;  // chunk slot -> slot of the caller's list (nullptr: identity); the
+                                   // megakernel's tail chunks (sp_mega.hpp) map slot k to order[k]
 };
 
 int        chunk_blocks_per_cu(size_t lds_bytes);
 hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int n_cu, hipStream_t stream);
+// ck_sum alone: image(p) from the per-sample radiance a.L, written at the slots a.slot_map names
+hipError_t chunk_sum(const Scene& sc, const ChunkArgs& a, hipStream_t stream);
 
 } // namespace spd

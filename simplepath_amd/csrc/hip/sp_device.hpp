@@ -167,6 +167,25 @@ __host__ __device__ inline size_t mt_off(int k) { return (size_t)(k / MT_BLK) * 
 __host__ __device__ inline int rsqrt_words(const Scene& sc) { return RSQ_HDR + (sc.rsqrt_shift ? (1 << sc.rsqrt_bits) : (2 << sc.rsqrt_bits)); }
 
 
+// Tail chunks of the DirectLighting megakernel (sp_mega.hpp tail_prep / tail_chunk): the K most
+// expensive tiles of the tile order (order[0 .. K)) are rendered as sample chunks at the END of the
+// persistent queue, so the frame's last work items are a few samples of one tile instead of whole
+// tiles.  Queue: items [0, K) prepare those tiles (camera rays, draw counts, every generation of
+// each pixel's stream into a store), items [K, num_tiles) are the other tiles as before, items
+// [num_tiles, num_tiles + K * chunks) shade one chunk each; sp_chunk.hip chunk_sum adds each pixel's
+// samples in order afterwards.  n_prep == 0: no tail chunks.
+struct TailArgs {
+    int64_t   n_prep;      // K
+    int64_t   n_items;     // K * chunks
+    uint32_t  chunks, chunk_len, gens_per_px;
+    size_t    n_px;        // K * 64 pixel slots (chunk slot k = queue item k)
+    float4*   hits;        // [spp][n_px] camera hit {t, code, beta, gamma}; code 0xffffffff = none
+    float*    L;           // [spp][3][n_px] per-sample radiance
+    uint64_t* gens;        // [K][gens_per_px] generation buffers (mt_off layout), generation g in buffer g
+    uint32_t* snap_ctl;    // [chunks][n_px] stream position at each chunk start: idx | gen << 16
+    uint32_t* ready;       // [K] 1 once tile k's prep item has published its store (zeroed per render)
+};
+
 struct RenderArgs {
     float*          out;        // tile-packed radiance
     const int32_t*  tile_ids;   // nullptr => identity
@@ -182,6 +201,10 @@ struct RenderArgs {
     unsigned long long* tile_diag; // SP_TILE_DIAG: per slot {t0, t1 (s_memrealtime), wave, item, 4 stage clocks}
     const int32_t*  order;      // queue position -> tile slot (nullptr: slot order); sp_mega.hip tile_order
     float*          tile_time;  // probe pass: per slot, the wave's time for the tile; no radiance written
+    // sp_tail_kernel only: the queue's prep and chunk item counts, and the rest of TailArgs in
+    // device memory (read per item: kernel arguments held across the persistent loop cost SGPRs)
+    int64_t         tail_prep, tail_items;
+    const TailArgs* tail;
 };
 
 } // namespace spd

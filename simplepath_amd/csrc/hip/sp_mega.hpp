@@ -21,6 +21,145 @@ __device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
     else return integrate_direct(c, ray);
 }
 
+// ------------------------------------------------------------------------------ tail chunks
+// (RenderArgs::tail, sp_device.hpp).  Why: a tile's 64 pixels run their 256-sample stream chains in
+// one wave, so the frame's last work items are whole tiles, whose durations move by ~20 % with
+// what the other waves on their SIMD do -- no cost estimate can order that noise away (DESIGN.md
+// §11l: bunny ends at 262.2 ms against 246.5 ms of work per wave).  The K most expensive tiles are
+// cut into sample chunks (the sample-chunk pipeline's scheme, sp_chunk.hip) whose shading comes
+// last in the queue, where short items fill the waves that would otherwise idle.  Same stream words
+// and floating-point sequence per sample, and the samples are summed in order (chunk_sum): the
+// image and the ray / draw counts are the megakernel's bit for bit.
+
+// PerspectiveCamera::generate_ray_impl of sample i (the sample loop below and sp_chunk.hip)
+__device__ __forceinline__ Ray tail_camera_ray(const Scene& sc, uint32_t px, uint32_t py, uint32_t i, const Rsq& q)
+{
+    const uint32_t seed2d = ((px << 16u) | py) ^ 0x6184faf4u;
+    const float    sx     = rseq_component(seed2d, sc.alpha2_0, i);
+    const float    sy     = rseq_component(seed2d, sc.alpha2_1, i);
+    const float    fx     = (float)(int)px + sx;
+    const float    fy     = (float)(int)py + sy;
+    Ray            ray;
+    ray.o = sc.camera.p;
+    ray.d = normalize(add(add(scale(fx, sc.camera.vx), scale(fy, sc.camera.vy)), sc.camera.vz), q);
+    return ray;
+}
+
+// Prep item k (queue item k < K): tile order[k]'s camera rays (Integrator.cpp:277-283: intersect
+// lights, then geometry) for every sample, their hit records and the radiance of light-only hits;
+// each sample's draw count (sample_draws) summed into the stream position at every chunk start;
+// then every generation of each pixel's stream, twisted once, into the store (sp_chunk.hip ck_camera
+// + ck_count in one item).  Publishes the store with an agent-scope release before setting
+// ready[k] (MI355X guide: stores, vmcnt(0), release, vmcnt(0), flag).
+__device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& args, const Rsq& q, Stack& st, int64_t k,
+                                          uint32_t lane, uint32_t dx, uint32_t dy, uint32_t& rays_total,
+                                          uint32_t& samples_total)
+{
+    const TailArgs& ta     = *args.tail;
+    const int64_t   slot   = args.order[k];
+    const int32_t   tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
+    const uint32_t  px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
+    const uint32_t  py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
+    const bool      inside = px < (uint32_t)sc.width && py < (uint32_t)sc.height;
+    const size_t    p      = (size_t)k * 64 + lane;
+    Rng             rng;
+    rng.lin  = 1; // generation g in buffer g of the pixel's store
+    rng.base = ta.gens + (size_t)k * ta.gens_per_px * MT_GEN_WORDS + (size_t)lane * MT_BLK;
+    // main.cpp:73; generation 0 (the seeded state) is never drawn from: the seed writes generation 1
+    if (inside) rng_seed_twisted(rng, ((px << 16u) | py) ^ 0xb0ae9d99u);
+    uint32_t T = 0; // stream position (words drawn) before sample i
+    for (uint32_t i = 0; i < args.spp; ++i) {
+        if (i % ta.chunk_len == 0) { // the lazy-switch form rng_skip leaves (sp_chunk.hip ck_count)
+            const uint32_t g = T ? (T - 1) / MT_N + 1 : 0u;
+            const uint32_t w = T ? T - (g - 1) * MT_N : (uint32_t)MT_N;
+            ta.snap_ctl[(size_t)(i / ta.chunk_len) * ta.n_px + p] = w | (g << 16);
+        }
+        float4   rec = make_float4(0.0f, __uint_as_float(0xffffffffu), 0.0f, 0.0f);
+        rgb      L   = mkc(0, 0, 0);
+        uint32_t nd  = 0;
+        if (inside && sc.max_depth > 0) {
+            const Ray      ray = tail_camera_ray(sc, px, py, i, q);
+            const LightHit lh  = scene_intersect_lights(sc, ray, k_ray_epsilon, k_infinite, st);
+            const Hit      h   = scene_intersect(sc, ray, k_ray_epsilon, lh.hit ? lh.t : k_infinite, st);
+            if (h.code != 0xffffffffu) {
+                rec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
+                nd  = sample_draws(sc, finish_hit(sc, h, ray, q), neg(ray.d), q);
+            } else if (lh.hit) {
+                L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, q)));
+            }
+        }
+        ta.hits[(size_t)i * ta.n_px + p]          = rec;
+        ta.L[((size_t)i * 3 + 0) * ta.n_px + p] = L.r;
+        ta.L[((size_t)i * 3 + 1) * ta.n_px + p] = L.g;
+        ta.L[((size_t)i * 3 + 2) * ta.n_px + p] = L.b;
+        T += nd;
+    }
+    if (inside) {
+        const uint32_t G = T ? (T - 1) / MT_N + 1 : 0u;
+#pragma unroll 1
+        for (uint32_t g = 1; g < G; ++g) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(rng, (int)g), mt_buf(rng, (int)g + 1));
+        if (sc.max_depth > 0) rays_total += args.spp; // the camera rays (trace() counts them)
+        samples_total += args.spp;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(ta.ready + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Chunk item j (queue item num_tiles + j): samples [c len, (c + 1) len) of tile order[k], k = j /
+// chunks, from the chunk's stream position in the store (no twisting: every generation is there),
+// direct_nee on the stored hit (sp_chunk.hip ck_shade); each sample's radiance into L.  Waits for
+// prep item k (taken before any chunk item: the queue is one counter, so its wave is running).
+__device__ __forceinline__ void tail_chunk(const Scene& sc, const RenderArgs& args, const Rsq& q, Stack& st, int64_t j,
+                                           uint32_t lane, uint32_t dx, uint32_t dy, uint32_t& rays_total,
+                                           uint32_t& shadow_total, uint32_t& draws_total)
+{
+    const TailArgs& ta = *args.tail;
+    const int64_t   k  = j / ta.chunks;
+    const uint32_t  c  = (uint32_t)(j % ta.chunks);
+    if (lane == 0)
+        while (__hip_atomic_load(ta.ready + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(4);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int64_t  slot   = args.order[k];
+    const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
+    const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
+    const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
+    const bool     inside = px < (uint32_t)sc.width && py < (uint32_t)sc.height;
+    const size_t   p      = (size_t)k * 64 + lane;
+    const uint32_t i0     = c * ta.chunk_len;
+    const uint32_t i1     = min(args.spp, i0 + ta.chunk_len);
+    if (!inside || i0 >= i1) return;
+    const uint32_t snap = ta.snap_ctl[(size_t)c * ta.n_px + p];
+    Rng            rng;
+    rng.base  = ta.gens + (size_t)k * ta.gens_per_px * MT_GEN_WORDS + (size_t)lane * MT_BLK;
+    rng.idx   = (int)(snap & 0xffffu);
+    rng.cur   = (int)(snap >> 16);
+    rng.lin   = 1;
+    rng.pre   = 1; // every generation is in the store: a buffer switch never twists
+    rng.ready = 1;
+    rng.draws = 0;
+    rng.pfn   = 0;
+    Ctx ctx{ sc, rng, q, st, 0u, 0u };
+    for (uint32_t i = i0; i < i1; ++i) {
+        rng_prepare(rng);
+        const float4   rec  = ta.hits[(size_t)i * ta.n_px + p];
+        const uint32_t code = __float_as_uint(rec.y);
+        if (code == 0xffffffffu) continue; // miss or light-only hit: L was stored by the prep item
+        const Ray   ray = tail_camera_ray(sc, px, py, i, q);
+        const Hit   h{ rec.x, code, rec.z, rec.w };
+        const Isect is  = finish_hit(sc, h, ray, q);
+        const rgb   L   = direct_nee(ctx, is, neg(ray.d));
+        ta.L[((size_t)i * 3 + 0) * ta.n_px + p] = L.r;
+        ta.L[((size_t)i * 3 + 1) * ta.n_px + p] = L.g;
+        ta.L[((size_t)i * 3 + 2) * ta.n_px + p] = L.b;
+    }
+    rays_total += ctx.rays;
+    shadow_total += ctx.shadow;
+    draws_total += rng.draws;
+}
+
 // Persistent kernel: 4 waves per block share the LDS RSQRTSS table; each wave independently
 // pulls 8x8 tiles from the queue (TileScheduler::get_next_tile) and owns one MT state slot.
 // One instantiation per integrator so each carries only its own live state; MINW is the
@@ -28,7 +167,8 @@ __device__ __forceinline__ rgb integrate(Ctx& c, Ray ray)
 // PROBE: the tile-order probe pass (sp_mega.hip) -- the same code writing each tile's wave time
 // to args.tile_time instead of radiance, compiled as its own kernel (sp_probe_kernel) so that
 // profiles list the probe and the render apart.
-template <int INTEG, bool PROBE>
+// TAIL: the DirectLighting render with tail chunks (sp_tail_kernel; queue layout in TailArgs).
+template <int INTEG, bool PROBE, bool TAIL = false>
 __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderArgs& args)
 {
     extern __shared__ uint32_t lds[];
@@ -63,7 +203,20 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
         int grabbed = 0;
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
         const int64_t item = __shfl(grabbed, 0, 64);
-        if (item >= args.num_tiles) break;
+        if constexpr (TAIL) {
+            if (item >= args.num_tiles + args.tail_items) break;
+            if (item < args.tail_prep) {
+                tail_prep(sc, args, q, st, item, (uint32_t)lane, dx, dy, rays_total, samples_total);
+                continue;
+            }
+            if (item >= args.num_tiles) {
+                tail_chunk(sc, args, q, st, item - args.num_tiles, (uint32_t)lane, dx, dy, rays_total, shadow_total,
+                           draws_total);
+                continue;
+            }
+        } else if (item >= args.num_tiles) {
+            break;
+        }
         const int64_t  slot    = args.order ? args.order[item] : item;
         const uint64_t t_start = (PROBE || args.tile_diag) ? __builtin_amdgcn_s_memrealtime() : 0;
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
@@ -155,6 +308,11 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_probe_kernel(Sc
 {
     render_tiles_body<INTEG, true>(sc, args);
 }
+template <int MINW>
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_tail_kernel(Scene sc, RenderArgs args)
+{
+    render_tiles_body<SP_INTEGRATOR_DIRECT_LIGHTING, false, true>(sc, args);
+}
 } // inline namespace SPD_LAYOUT_NS
 
 using KernelFn = void (*)(Scene, RenderArgs);
@@ -165,6 +323,7 @@ KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 KernelFn probe_direct(int variant); // nullptr: no probe kernel (queue order)
 KernelFn probe_rrnee(int waves);
+KernelFn tail_direct(); // DirectLighting with tail chunks, 4 waves per SIMD (sp_mega_tail.hip)
 hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
                              hipStream_t stream);
 

@@ -1,0 +1,16 @@
+// sp_mega_tail.hip -- the DirectLighting megakernel with tail chunks (sp_mega.hpp tail_prep /
+// tail_chunk, sp_device.hpp TailArgs), built with sp_mega_direct.hip's settings: no draw-ahead
+// window, the glossy estimate's words touched in advance, paired draws.  4 waves per SIMD only
+// (the render's default variant; other requested variants render without tail chunks).
+#define SP_RNG_PF 0
+#ifndef SP_RHO_TOUCH
+#define SP_RHO_TOUCH 1
+#endif
+#ifndef SP_RNG_PAIR
+#define SP_RNG_PAIR 1
+#endif
+#include "sp_mega.hpp"
+
+namespace spd {
+KernelFn tail_direct() { return sp_tail_kernel<4>; }
+} // namespace spd

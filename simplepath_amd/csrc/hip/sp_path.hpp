@@ -2626,6 +2626,31 @@ __device__ __forceinline__ rgb direct_nee(Ctx& c, const Isect& is, f3 wo)
     return L;
 }
 
+// Stream words one direct_nee call at hit `is` draws: two per light for Light::sample, plus 32
+// for the glossy rho estimate of Material::eval when the light sample is usable and wo.y != 0 in
+// the shading frame.  For sphere and uniform environment lights usability (pdf != 0, L not black)
+// does not depend on the drawn numbers -- pdf is sphere_pdf(observer) or a constant, L the
+// radiance -- so the count is known from the hit (the sample chunks, sp_chunk.hip, and the
+// megakernel's tail chunks, sp_mega.hpp; not used with an image light).
+__device__ __forceinline__ uint32_t sample_draws(const Scene& sc, const Isect& is, f3 wo, const Rsq& q)
+{
+    const Material& m    = sc.materials[is.material];
+    const int       base = (m.kind == SP_MAT_CLEARCOAT) ? sc.materials[m.base].kind : m.kind;
+    bool            rho  = false;
+    if (base != SP_MAT_LAMBERTIAN) {
+        const Onb o = onb_from_v(is.n, q);
+        rho         = to_onb(o, wo).y != 0.0f;
+    }
+    uint32_t n = 0;
+    for (int li = 0; li < sc.n_lights; ++li) {
+        const Light lt  = uload_light(sc.lights + li);
+        const float pdf = (lt.kind == SP_LIGHT_SPHERE) ? sphere_pdf(lt, is.p) : k_uniform_sphere_pdf;
+        n += 2;
+        if (rho && !(pdf == 0.0f || cblack(lt.radiance))) n += 32;
+    }
+    return n;
+}
+
 __device__ __forceinline__ rgb integrate_direct(Ctx& c, Ray ray)
 {
     rgb L = mkc(0, 0, 0);
