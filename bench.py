@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--pipeline", default="auto", choices=["auto", "megakernel", "wavefront", "chunks"])
     ap.add_argument("--waves", type=int, default=0,
                     help="megakernel occupancy variant (sp_render_params.waves_per_simd; 0 = automatic)")
+    ap.add_argument("--tail-fraction", type=float, default=0.0,
+                    help="megakernel tail chunks (sp_render_params.tail_fraction): 0 automatic, < 0 off, else the fraction")
     ap.add_argument("--tile-order-factor", type=float, default=0.0,
                     help="megakernel tile order (sp_render_params.tile_order_factor): 0 automatic, > 0 always, < 0 queue order")
     ap.add_argument("--per-lane-queries", action="store_true",
@@ -258,7 +260,8 @@ def main():
             return _CpuStats(st, (time.perf_counter() - t) * 1e3)
         return sp.render_tiles_device(scene, integ, args.spp, my_tiles, out.data_ptr(), stream,
                                       pipeline=args.pipeline, stage_timing=True, waves_per_simd=args.waves,
-                                      per_lane_queries=args.per_lane_queries, tile_order_factor=args.tile_order_factor)
+                                      per_lane_queries=args.per_lane_queries, tile_order_factor=args.tile_order_factor,
+                                      tail_fraction=args.tail_fraction)
 
     def step():
         st = render()
@@ -418,7 +421,7 @@ def sim_all_ranks(args, scene, integ, n_tiles, rdev):
         def render():
             return sp.render_tiles_device(scene, integ, args.spp, tiles, out.data_ptr(), stream, pipeline=args.pipeline,
                                           stage_timing=True, waves_per_simd=args.waves,
-                                          tile_order_factor=args.tile_order_factor)
+                                          tile_order_factor=args.tile_order_factor, tail_fraction=args.tail_fraction)
         for _ in range(args.warmup):
             render()
         torch.cuda.synchronize()
@@ -542,16 +545,21 @@ def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
         probe_ms = sum(s.stage_ms[1] for s in stats) / n
         if not render_ms > 0:
             render_ms, probe_ms = kernel_ms, 0.0
+        # with tail chunks (sp_render_stats.tail_tiles > 0) the render kernel is sp_tail_kernel, and
+        # the same events also hold chunk_sum (ck_sum, ~0.1 ms).  The algorithmic bytes stay the
+        # frame's (the tail tiles' hit records and per-sample radiance are not counted: the same
+        # frame, the same bytes, whichever way it is scheduled)
+        kname = "sp_tail_kernel" if st.tail_tiles > 0 else "sp_render_kernel"
         alg = st.rng_draws * MT_BYTES_PER_DRAW + pixels * PIXEL_BYTES + scene_bytes
         achieved = alg / (render_ms * 1e-3) / 1e9
-        if tj is not None and "sp_render_kernel" in tj.get("kernels", {}):
-            traffic = tj["kernels"]["sp_render_kernel"]["hbm_bytes_per_launch"]
+        if tj is not None and kname in tj.get("kernels", {}):
+            traffic = tj["kernels"][kname]["hbm_bytes_per_launch"]
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "sp_render_kernel",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
                 "traffic_source": traffic_source(args, tj),
-                "scene_bytes": scene_bytes,
+                "scene_bytes": scene_bytes, "tail_tiles": st.tail_tiles, "tail_chunks": st.tail_chunks,
                 "kernel_ms": round(render_ms, 3), "probe_ms": round(probe_ms, 3), "alg_bytes_per_launch": alg,
-                "valu": valu_of(args, "sp_render_kernel")}
+                "valu": valu_of(args, kname)}
     names = ["wf_init+wf_resolve", "wf_primary", "wf_shade", "wf_shadow"]
     tot = [sum(s.stage_ms[k] for s in stats) / n for k in range(4)]
     spp = args.spp

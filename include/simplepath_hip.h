@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 5
+#define SP_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------------- */
 enum {
@@ -226,7 +226,16 @@ typedef struct sp_render_params {
                                          columns left and right, and the tile below when k divides
                                          the tile columns); any other list uses each tile's own
                                          probe time.                                                  */
-    int32_t        reserved[2];       /* must be 0                                                  */
+    /* ---- ABI 6 ---- */
+    float          tail_fraction;     /* megakernel tail chunks (DirectLighting at 3 or 4 waves per SIMD,
+                                         with the tile order and draw counts known from the camera
+                                         hits -- no image light):
+                                         the most expensive tail_fraction x n_tiles tiles of the
+                                         order are rendered as sample chunks at the end of the
+                                         persistent queue, so the frame ends on short work items
+                                         (identical image and counts).  0 = automatic (0.12 where
+                                         it applies), < 0 off, else (0, 1].                         */
+    int32_t        reserved;          /* must be 0                                                  */
 } sp_render_params;
 
 /* Device pipeline selection (sp_render_params.flags).  All produce identical images. */
@@ -275,6 +284,8 @@ typedef struct sp_render_stats {
                               /* the render kernel, [1] the tile-order probe + partition           */
     int32_t  parts;           /* wavefront: concurrent parts (streams); part 0 holds ceil(tiles/2) */
     int32_t  stack_depth;     /* traversal-stack entries per lane the BVH walks needed (ABI 3)      */
+    int32_t  tail_tiles;      /* megakernel: tiles rendered as tail chunks (ABI 6; 0: none)         */
+    int32_t  tail_chunks;     /* ... and sample chunks per such tile                                */
 } sp_render_stats;
 
 /* BVH statistics (sp_scene_bvh_build_info).  depth = levels below the root of the binary BVH

@@ -50,6 +50,8 @@ class RenderStats:
     stage_ms: tuple = (0.0, 0.0, 0.0, 0.0)
     parts: int = 1
     stack_depth: int = 0
+    tail_tiles: int = 0   # megakernel: tiles rendered as tail chunks (ABI 6)
+    tail_chunks: int = 0  # ... sample chunks per such tile
 
 
 class Scene:
@@ -196,7 +198,7 @@ PER_LANE_QUERIES = 8  # SP_RENDER_PER_LANE_QUERIES (ABI 5)
 
 def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeline="auto",
             stage_timing=False, waves_per_simd=0, chunks_per_pixel=0, chunk_max_gb=0.0,
-            tile_order_factor=0.0, per_lane_queries=False) -> tuple:
+            tile_order_factor=0.0, per_lane_queries=False, tail_fraction=0.0) -> tuple:
     if isinstance(integrator, str):
         integrator = string_to_integrator_type(integrator)
     p = _abi.sp_render_params()
@@ -214,12 +216,13 @@ def _params(integrator, spp, tile_ids: Optional[np.ndarray], stream=None, pipeli
     p.chunks_per_pixel = int(chunks_per_pixel)
     p.chunk_max_gb = float(chunk_max_gb)
     p.tile_order_factor = float(tile_order_factor)
+    p.tail_fraction = float(tail_fraction)
     return p, keep
 
 
 def _stats(s: _abi.sp_render_stats) -> RenderStats:
     return RenderStats(s.rays, s.shadow_rays, s.samples, s.rng_draws, s.kernel_ms, s.pipeline, s.launches,
-                       s.primary_hits, tuple(s.stage_ms), s.parts, s.stack_depth)
+                       s.primary_hits, tuple(s.stage_ms), s.parts, s.stack_depth, s.tail_tiles, s.tail_chunks)
 
 
 def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Optional[Sequence[int]] = None,
@@ -227,6 +230,7 @@ def render_tiles(scene: Scene, integrator, num_pixel_samples: int, tile_ids: Opt
     """Render tiles on the GPU; returns (tile-packed radiance [n,64,3] float32, RenderStats).
     options: waves_per_simd, chunks_per_pixel, chunk_max_gb (sp_render_params, ABI 4),
     tile_order_factor (ABI 5: 0 automatic, > 0 forced with that factor, < 0 queue order),
+    tail_fraction (ABI 6: megakernel tail chunks, 0 automatic, < 0 off, else the fraction of tiles),
     per_lane_queries (ABI 5: IterativeRRNEE without the merged query pass -- the comparison path)."""
     p, keep = _params(integrator, num_pixel_samples, None if tile_ids is None else np.asarray(tile_ids),
                       pipeline=pipeline, **options)

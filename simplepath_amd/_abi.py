@@ -96,7 +96,9 @@ class sp_render_params(C.Structure):
         ("d_tile_ids", C.c_void_p), ("waves_per_simd", C.c_int32), ("chunks_per_pixel", C.c_int32),
         ("chunk_max_gb", C.c_float),
         # ABI 5
-        ("tile_order_factor", C.c_float), ("reserved", C.c_int32 * 2),
+        ("tile_order_factor", C.c_float),
+        # ABI 6
+        ("tail_fraction", C.c_float), ("reserved", C.c_int32),
     ]
 
 
@@ -113,7 +115,7 @@ class sp_render_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
                 ("rng_draws", C.c_uint64), ("kernel_ms", C.c_float), ("pipeline", C.c_int32),
                 ("launches", C.c_int32), ("primary_hits", C.c_uint64), ("stage_ms", C.c_float * 4),
-                ("parts", C.c_int32), ("stack_depth", C.c_int32)]
+                ("parts", C.c_int32), ("stack_depth", C.c_int32), ("tail_tiles", C.c_int32), ("tail_chunks", C.c_int32)]
 
 
 class sp_bvh_info(C.Structure):

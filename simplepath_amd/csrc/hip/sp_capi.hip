@@ -26,8 +26,8 @@ hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float fact
 bool       has_probe(int integ);
 hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
                         hipStream_t stream);
-hipError_t launch_tail(const Scene& sc, const RenderArgs& args, int blocks, size_t lds_bytes, hipStream_t stream);
-int        tail_blocks_per_cu(size_t lds_bytes);
+hipError_t launch_tail(const Scene& sc, const RenderArgs& args, int variant, int blocks, size_t lds_bytes, hipStream_t stream);
+int        tail_blocks_per_cu(int variant, size_t lds_bytes);
 } // namespace spd
 
 namespace {
@@ -943,10 +943,10 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
 // Megakernel tail chunks (render_tiles_impl): the fraction of the tiles cut into sample chunks at
 // the end of the queue, and chunks per tile.
 #ifndef SP_TAIL_FRAC
-#define SP_TAIL_FRAC 0.0f
+#define SP_TAIL_FRAC 0.12f
 #endif
 #ifndef SP_TAIL_CHUNKS
-#define SP_TAIL_CHUNKS 32
+#define SP_TAIL_CHUNKS 64
 #endif
 
 // Sample-chunk buffer plan (sp_chunk.hip): the same sizes decide AUTO and are allocated.
@@ -1017,8 +1017,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     if (!s || !p || !d_out) return fail(SP_ERR_ARG, "null argument");
     if (s->device < 0) return fail(SP_ERR_STATE, "sp_scene_upload must be called before sp_render_tiles");
     if (p->samples_per_pixel == 0) return fail(SP_ERR_ARG, "samples_per_pixel must be > 0");
-    for (int32_t r : p->reserved)
-        if (r != 0) return fail(SP_ERR_ARG, "sp_render_params.reserved must be 0");
+    if (p->reserved != 0) return fail(SP_ERR_ARG, "sp_render_params.reserved must be 0");
+    if (!(p->tail_fraction <= 1.0f)) return fail(SP_ERR_ARG, "tail_fraction must be at most 1 (and not NaN)");
     if (p->tile_ids && p->d_tile_ids) return fail(SP_ERR_ARG, "give tile_ids (host) or d_tile_ids (device), not both");
     if (p->chunks_per_pixel < 0) return fail(SP_ERR_ARG, "chunks_per_pixel < 0");
     if (!(p->chunk_max_gb >= 0.0f)) return fail(SP_ERR_ARG, "chunk_max_gb < 0");
@@ -1143,6 +1143,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     }
     SP_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream));
     int launches = 0, parts_used = 1;
+    int64_t tail_k = 0;  // megakernel tail chunks: tiles cut (tail_ch chunks each)
+    int     tail_ch = 0;
     if (pipeline == SP_PIPELINE_WAVEFRONT) {
         const size_t stack_lds = (size_t)4 * s->dev.stack_words * 64 * 4;
         if (stack_lds > 160 * 1024) return fail(SP_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
@@ -1412,18 +1414,21 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         }
         // Tail chunks (sp_mega.hpp, sp_device.hpp TailArgs): the K = tail_frac x n_tiles most
         // expensive tiles of the order are rendered as sample chunks at the end of the queue.
-        // DirectLighting at 4 waves per SIMD with the tile order and draw counts known from the
+        // DirectLighting at 3 or 4 waves per SIMD with the tile order and draw counts known from the
         // camera hits (no image light); SP_TAIL_FRAC (0: off) and SP_TAIL_CHUNKS override.
-        int64_t        tail_k = 0;
         spd::ChunkArgs tail_sum{};
-        if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && variant == 4 && a.order) {
+        if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && (variant == 3 || variant == 4) && a.order) {
+            // automatic: SP_TAIL_FRAC, or the environment's SP_TAIL_FRAC (A/B runs); the caller's
+            // tail_fraction when set (< 0: off)
             float tail_frac = SP_TAIL_FRAC;
-            int   tail_ch   = SP_TAIL_CHUNKS;
+            tail_ch         = SP_TAIL_CHUNKS;
             if (const char* v = std::getenv("SP_TAIL_FRAC")) tail_frac = (float)std::atof(v);
             if (const char* v = std::getenv("SP_TAIL_CHUNKS")) tail_ch = std::atoi(v);
+            if (p->tail_fraction != 0.0f) tail_frac = p->tail_fraction;
             const ChunkPlan tp = chunk_plan(s, 1, spp_u, std::max(1, tail_ch));
             if (tail_frac > 0.0f && tp.known_draws) {
-                tail_k = std::min<int64_t>(n_tiles, std::max<int64_t>(1, (int64_t)std::ceil((double)tail_frac * (double)n_tiles)));
+                // ceil(frac x n), with frac the f32 caller value (0.05f x 5120 = 256.0000038: 256 tiles)
+                tail_k = std::min<int64_t>(n_tiles, std::max<int64_t>(1, (int64_t)std::ceil((double)tail_frac * (double)n_tiles - 1e-3)));
                 const ChunkPlan cp    = chunk_plan(s, tail_k, spp_u, std::max(1, tail_ch));
                 const size_t    a_hdr = 256, a_rdy = ((size_t)tail_k * 4 + 255) / 256 * 256;
                 const size_t    need  = a_hdr + a_rdy + cp.b_hits + cp.b_L + cp.b_snap + cp.b_ctl;
@@ -1436,6 +1441,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                 }
                 char*         base = static_cast<char*>(s->tail_buf);
                 spd::TailArgs ta{};
+                tail_ch        = (int)cp.chunks;
                 ta.n_prep      = tail_k;
                 ta.n_items     = tail_k * cp.chunks;
                 ta.chunks      = (uint32_t)cp.chunks;
@@ -1469,10 +1475,10 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             SP_HIP(hipEventRecord(s->ev_render, stream));
         }
         if (tail_k > 0) {
-            const int     t_per_cu = spd::tail_blocks_per_cu(lds_bytes);
+            const int     t_per_cu = spd::tail_blocks_per_cu(variant, lds_bytes);
             const int64_t t_need   = (n_tiles + a.tail_items + 3) / 4;
             const int     t_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * t_per_cu, t_need));
-            SP_HIP(spd::launch_tail(sc_run, a, t_blocks, lds_bytes, stream));
+            SP_HIP(spd::launch_tail(sc_run, a, variant, t_blocks, lds_bytes, stream));
             SP_HIP(spd::chunk_sum(sc_run, tail_sum, stream));
             launches += 1;
         } else {
@@ -1529,6 +1535,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         stats->primary_hits = c[4];
         stats->parts        = parts_used;
         stats->stack_depth  = s->dev.stack_depth;
+        stats->tail_tiles   = (int32_t)tail_k;
+        stats->tail_chunks  = tail_k > 0 ? tail_ch : 0;
         if (pipeline == SP_PIPELINE_MEGAKERNEL && timing) { // [0] the render kernel, [1] probe + tile order
             float r = ms;
             if (s->ev_render) SP_HIP(hipEventElapsedTime(&r, s->ev_render, s->ev1));

@@ -323,7 +323,7 @@ KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 KernelFn probe_direct(int variant); // nullptr: no probe kernel (queue order)
 KernelFn probe_rrnee(int waves);
-KernelFn tail_direct(); // DirectLighting with tail chunks, 4 waves per SIMD (sp_mega_tail.hip)
+KernelFn tail_direct(int variant); // DirectLighting with tail chunks, 3 or 4 waves per SIMD (sp_mega_tail.hip)
 hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
                              hipStream_t stream);
 

@@ -1,7 +1,8 @@
 // sp_mega_tail.hip -- the DirectLighting megakernel with tail chunks (sp_mega.hpp tail_prep /
 // tail_chunk, sp_device.hpp TailArgs), built with sp_mega_direct.hip's settings: no draw-ahead
-// window, the glossy estimate's words touched in advance, paired draws.  4 waves per SIMD only
-// (the render's default variant; other requested variants render without tail chunks).
+// window, the glossy estimate's words touched in advance, paired draws.  4 waves per SIMD (the
+// render's default) and 3 (the default where a deep BVH's LDS stacks cap the occupancy); other
+// requested variants render without tail chunks.
 #define SP_RNG_PF 0
 #ifndef SP_RHO_TOUCH
 #define SP_RHO_TOUCH 1
@@ -12,5 +13,5 @@
 #include "sp_mega.hpp"
 
 namespace spd {
-KernelFn tail_direct() { return sp_tail_kernel<4>; }
+KernelFn tail_direct(int variant) { return variant == 3 ? sp_tail_kernel<3> : sp_tail_kernel<4>; }
 } // namespace spd

@@ -58,11 +58,13 @@ def test_abi_version_and_struct_layout():
     # serialisation of renders.
     import ctypes as C
     text = open(HEADER).read()
-    assert re.search(r"#define SP_ABI_VERSION 5\b", text)
-    assert C.sizeof(_abi.sp_render_params) == 72  # gcc on include/simplepath_hip.h: 72, 40, 60, 32
+    # ABI 6: tail_fraction takes the first reserved word (same size); the stats grew two words.
+    assert re.search(r"#define SP_ABI_VERSION 6\b", text)
+    assert C.sizeof(_abi.sp_render_params) == 72  # gcc on include/simplepath_hip.h: 72, 40, 60, 64, 68, 32, 88
     assert _abi.sp_render_params.d_tile_ids.offset == 40 and _abi.sp_render_params.tile_order_factor.offset == 60
-    assert _abi.sp_render_params.reserved.offset == 64
+    assert _abi.sp_render_params.tail_fraction.offset == 64 and _abi.sp_render_params.reserved.offset == 68
     assert C.sizeof(_abi.sp_upload_params) == 32
+    assert C.sizeof(_abi.sp_render_stats) == 88
 
 
 def test_upload_params_validated_before_the_device(scene_dir):

@@ -111,12 +111,9 @@ def test_render_params_validation(scene_dir):
     with pytest.raises(sp.SimplePathError):
         sp.render_tiles(s, "direct_lighting", 1, chunks_per_pixel=-2)
     import ctypes as C
-    for field, value in (("reserved", 1), ("flags", 64)):
+    for field, value in (("reserved", 1), ("flags", 64), ("tail_fraction", 1.5), ("tail_fraction", float("nan"))):
         p, keep = sp._params("direct_lighting", 1, None)
-        if field == "reserved":
-            p.reserved[0] = value
-        else:
-            p.flags = value
+        setattr(p, field, value)
         out = torch.zeros((16, 64, 3), dtype=torch.float32, device="cuda:0")
         rc = _abi.lib().sp_render_tiles(s.handle, C.byref(p), C.c_void_p(out.data_ptr()), None)
         assert rc == _abi.SP_ERR_ARG, field
@@ -153,7 +150,10 @@ def test_tile_order_probe_is_invisible(scene_dir, integrator):
     # forced (tile_order_factor): AUTO uses it from 6 tiles per wave and 128 spp (IterativeRRNEE: 4, 16)
     ref, rst = sp.render_tiles(s, integrator, 2, pipeline="megakernel", tile_order_factor=2.0)
     # probe, partition, render; integrators without a probe kernel (sp_probe_*.hip) keep queue order
-    assert rst.launches == (1 if integrator == "whitted" else 3)
+    # (+ the in-order sum of the tail chunks: DirectLighting with the order renders its most expensive
+    # tiles as sample chunks, tests/test_gpu_tail.py)
+    assert rst.launches == (1 if integrator == "whitted" else 3 + (rst.tail_tiles > 0))
+    assert (rst.tail_tiles > 0) == (integrator == "direct_lighting")
     off, ost = sp.render_tiles(s, integrator, 2, pipeline="megakernel", tile_order_factor=-1.0)
     assert ost.launches == 1
     assert np.array_equal(ref.view(np.uint32), off.view(np.uint32))
@@ -175,7 +175,8 @@ def test_tile_order_on_strided_lists(scene_dir, integrator):
     for k in (1, 2, 3, 4):
         ids = np.arange(k - 1, ref.shape[0], k, dtype=np.int32)
         sub, st = sp.render_tiles(s, integrator, 2, ids, pipeline="megakernel", tile_order_factor=2.0)
-        assert st.launches == 3, k  # the order ran: more tiles than persistent waves
+        assert st.launches == 3 + (st.tail_tiles > 0), k  # the order ran: more tiles than persistent waves
+        assert (st.tail_tiles > 0) == (integrator == "direct_lighting"), k
         assert np.array_equal(sub.view(np.uint32), ref[ids].view(np.uint32)), k
 
 

@@ -1,0 +1,104 @@
+"""The DirectLighting megakernel's tail chunks (sp_mega.hpp tail_prep / tail_chunk):
+the most expensive tiles of the tile order are rendered as sample chunks at the end of the
+persistent queue.  Only which wave computes which samples, and when, changes -- every sample sees
+the same stream words and floating-point sequence and each pixel's samples are summed in order --
+so images and ray / draw counts must equal the plain megakernel's bit for bit, and the CPU
+oracle's with the reference-order BVH (main.cpp:86-103: one tile's pixels x samples)."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import simplepath_amd as sp
+from simplepath_amd import scenes
+from tests import _oracle
+
+pytestmark = pytest.mark.gpu
+
+W, H = 640, 512  # 5120 tiles: more than the 4096 persistent waves, so the tile order can run
+
+
+def load(path, bvh=0, w=W, h=H):
+    s = sp.Scene.from_file(path)
+    s.set_resolution(w, h)
+    s.upload(device=0, bvh_mode=bvh)
+    return s
+
+
+def same_bits(a, b):
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def counts(st):
+    return (st.rays, st.shadow_rays, st.samples, st.rng_draws)
+
+
+@pytest.fixture
+def tail_chunks(monkeypatch):
+    def set_chunks(n):
+        monkeypatch.setenv("SP_TAIL_CHUNKS", str(n))
+    return set_chunks
+
+
+@pytest.mark.parametrize("spp", [3, 8])
+def test_tail_chunks_are_invisible(scene_dir, tail_chunks, spp):
+    s = load(os.path.join(scene_dir, "bunny.sp"))
+    n = sp.TileScheduler(W, H).get_num_tiles()
+    ref, rst = sp.render_tiles(s, "direct_lighting", spp, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=-1.0)
+    assert rst.tail_tiles == 0 and rst.launches == 3
+    for frac, chunks in ((0.05, 64), (0.12, 2), (0.5, 3), (1.0, 1)):
+        tail_chunks(chunks)
+        img, st = sp.render_tiles(s, "direct_lighting", spp, pipeline="megakernel", tile_order_factor=2.0,
+                                  tail_fraction=frac)
+        k = min(n, math.ceil(float(np.float32(frac)) * n - 1e-3))
+        len_ = -(-spp // min(chunks, spp))
+        assert st.tail_tiles == k and st.tail_chunks == -(-spp // len_), (frac, chunks)
+        assert st.launches == 4  # probe, partition, render with tail chunks, the in-order sum
+        assert counts(st) == counts(rst), (frac, chunks)
+        assert same_bits(img, ref), (frac, chunks)
+
+
+def test_tail_chunks_on_caller_lists(scene_dir):
+    # shuffled subsets and duplicate ids: chunk slot k maps to the list slot order[k], whose tile the
+    # caller named; a duplicated tile gets two slots (two stores), both equal to the frame's row
+    s = load(os.path.join(scene_dir, "bunny.sp"))
+    ref, _ = sp.render_tiles(s, "direct_lighting", 3, pipeline="megakernel", tile_order_factor=-1.0)
+    rng = np.random.default_rng(7)
+    ids = rng.permutation(ref.shape[0])[:4600].astype(np.int32)
+    ids = np.concatenate([ids, ids[:300]])  # 300 duplicates
+    sub, st = sp.render_tiles(s, "direct_lighting", 3, ids, pipeline="megakernel", tile_order_factor=2.0,
+                              tail_fraction=0.25)
+    assert st.tail_tiles == math.ceil(float(np.float32(0.25)) * ids.size - 1e-3)
+    assert same_bits(sub, ref[ids])
+
+
+def test_tail_chunks_match_the_oracle(scene_dir):
+    # reference-order BVH: the whole frame, tail tiles included, bit for bit with the CPU oracle
+    s = load(os.path.join(scene_dir, "bunny.sp"), bvh=1)
+    img, st = sp.render_tiles(s, "direct_lighting", 2, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=0.3)
+    assert st.tail_tiles > 0
+    c, cst = _oracle.render(s, sp.string_to_integrator_type("direct_lighting"), 2, variant="spm")
+    assert (st.rays, st.shadow_rays) == (cst["rays"], cst["shadow_rays"])
+    assert same_bits(img, c)
+
+
+def test_no_tail_chunks_with_an_image_light(scene_dir):
+    # with an image light a sample's draw count depends on the drawn numbers (Light::sample), so
+    # the camera pass cannot place the chunk starts: the frame renders without tail chunks
+    s = load(os.path.join(scene_dir, "material_spheres_ibl.sp"), w=640, h=512)
+    img, st = sp.render_tiles(s, "direct_lighting", 2, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=0.5)
+    assert st.tail_tiles == 0 and st.launches == 3
+    off, ost = sp.render_tiles(s, "direct_lighting", 2, pipeline="megakernel", tile_order_factor=-1.0)
+    assert same_bits(img, off) and counts(st) == counts(ost)
+
+
+@pytest.mark.parametrize("max_depth", [0, 1])
+def test_tail_chunks_max_depth(tmp_path, max_depth):
+    # max_depth 0: no camera ray is traced and nothing is drawn (integrate_direct returns black)
+    path = scenes.write_closed_room_scene(str(tmp_path), max_depth=max_depth, name=f"room_{max_depth}.sp")
+    s = load(path)
+    ref, rst = sp.render_tiles(s, "direct_lighting", 4, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=-1.0)
+    img, st = sp.render_tiles(s, "direct_lighting", 4, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=0.4)
+    assert st.tail_tiles > 0
+    assert counts(st) == counts(rst) and same_bits(img, ref)
