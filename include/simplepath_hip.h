@@ -211,8 +211,9 @@ typedef struct sp_render_params {
     float          tile_order_factor; /* megakernel tile order (DirectLighting, IterativeRRNEE): 0 =
                                          automatic (a one-sample probe times every tile; tiles
                                          slower than 2x the mean go first, then 24 cost classes a
-                                         quarter octave apart; from 6 tiles per wave and 128 spp,
-                                         IterativeRRNEE from 4 tiles per wave and 16 spp);
+                                         quarter octave apart; from 6 tiles per wave and 128 spp --
+                                         3 with tail chunks (ABI 6) --, IterativeRRNEE from 4 tiles
+                                         per wave and 16 spp);
                                          > 0: with this factor whenever it can apply; < 0: queue
                                          order.  It cannot apply, and the frame renders in queue
                                          order whatever the factor, when the megakernel does not
@@ -233,8 +234,11 @@ typedef struct sp_render_params {
                                          the most expensive tail_fraction x n_tiles tiles of the
                                          order are rendered as sample chunks at the end of the
                                          persistent queue, so the frame ends on short work items
-                                         (identical image and counts).  0 = automatic (0.12 where
-                                         it applies), < 0 off, else (0, 1].                         */
+                                         (identical image and counts).  0 = automatic: where it
+                                         applies, waves / n_tiles clamped to [0.12, 0.3] (and AUTO
+                                         then picks the megakernel from 3 tiles per persistent wave
+                                         and 128 spp, a 2-GPU shard of a 1080p frame included);
+                                         < 0 off, else (0, 1].                                      */
     int32_t        reserved;          /* must be 0                                                  */
 } sp_render_params;
 

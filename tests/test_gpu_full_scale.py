@@ -198,10 +198,11 @@ def test_full_scale_bunny_frame(bvh):
     ref = g["radiance"]
     frame, st = sp.render_tiles(s, "direct_lighting", int(g["spp"]))
     assert frame.shape[0] == 32400
-    # probe, partition, render, the in-order sum of the tail chunks: the 12 % most expensive tiles of
-    # the order (the 8 slowest golden tiles among them) are rendered as sample chunks
+    # probe, partition, render, the in-order sum of the tail chunks: the most expensive tiles of the
+    # order -- persistent waves / 32400 of them, at least 12 % (the 8 slowest golden tiles among
+    # them) -- are rendered as 64 sample chunks each
     assert st.pipeline == sp.PIPELINES["megakernel"] and st.launches == 4
-    assert st.tail_tiles == 3888 and st.tail_chunks == 64
+    assert 3888 <= st.tail_tiles <= 4096 and st.tail_chunks == 64
     assert st.stack_depth == expected_stack(built, bvh)
     out = frame[ids]
     r = rel_l2(out, ref)

@@ -102,3 +102,18 @@ def test_tail_chunks_max_depth(tmp_path, max_depth):
     img, st = sp.render_tiles(s, "direct_lighting", 4, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=0.4)
     assert st.tail_tiles > 0
     assert counts(st) == counts(rst) and same_bits(img, ref)
+
+
+def test_auto_takes_the_tail_on_a_two_way_shard(scene_dir):
+    # AUTO: DirectLighting from 3 tiles per persistent wave and 128 spp (no image light) runs the
+    # megakernel with its tile order and tail chunks -- a 2-GPU shard of the 1080p frame (16200
+    # tiles) included, which the sample chunks rendered before ABI 6; same image either way
+    from simplepath_amd import shard
+    s = load(os.path.join(scene_dir, "bunny.sp"), w=1920, h=1080)
+    ids = shard.shard_tiles(sp.TileScheduler(1920, 1080).get_num_tiles(), 0, 2)
+    img, st = sp.render_tiles(s, "direct_lighting", 128, ids)
+    assert st.pipeline == sp.PIPELINES["megakernel"] and st.tail_tiles > 0
+    ck, cst = sp.render_tiles(s, "direct_lighting", 128, ids, pipeline="chunks")
+    assert counts(st) == counts(cst) and same_bits(img, ck)
+    _, ost = sp.render_tiles(s, "direct_lighting", 8, ids, tail_fraction=-1.0)
+    assert ost.pipeline == sp.PIPELINES["chunks"]  # tail off (or below 128 spp): the old rule
