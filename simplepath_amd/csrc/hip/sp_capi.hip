@@ -948,6 +948,14 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
 #ifndef SP_TAIL_CHUNKS
 #define SP_TAIL_CHUNKS 64
 #endif
+// The sample-chunk pipeline's fused form (render_tiles_impl): on, and the preps placed ahead of the
+// first chunks = persistent waves / SP_CK_FRONT_DIV
+#ifndef SP_CK_FUSED
+#define SP_CK_FUSED 1
+#endif
+#ifndef SP_CK_FRONT_DIV
+#define SP_CK_FRONT_DIV 16
+#endif
 
 // Sample-chunk buffer plan (sp_chunk.hip): the same sizes decide AUTO and are allocated.
 struct ChunkPlan {
@@ -1305,10 +1313,74 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         a.counter     = s->ck_ctr;
         a.counters    = s->counters;
         a.out         = d_out;
+        // Fused form (known draw counts): ck_camera, then the counts and the shading in ONE persistent
+        // queue of the megakernel's tail kernel (sp_mega.hpp, RenderArgs::tail_front): each tile's
+        // prep (stream positions, generations into the store) runs P tiles ahead of its chunks, so the
+        // HBM-bound twists overlap the shading instead of running as a phase of their own (ck_count).
+        // Same store contents and chunk starts, same image.  SP_CK_FUSED=0: the four-kernel form.
+        bool fused = cp.known_draws && SP_CK_FUSED;
+        if (const char* v = std::getenv("SP_CK_FUSED")) fused = cp.known_draws && std::atoi(v) != 0;
         SP_HIP(hipMemsetAsync(s->ck_ctr, 0, 2 * sizeof(int32_t), stream));
-        SP_HIP(hipEventRecord(s->ev0, stream));
-        SP_HIP(spd::chunk_render(s->dev, a, blocks, s->n_cu, stream));
-        launches = 4;
+        if (fused) {
+            // the tail kernel's LDS (the megakernel's: RSQRTSS table + per-wave stacks) and occupancy
+            size_t lds_static = spd::render_static_lds(SP_INTEGRATOR_DIRECT_LIGHTING, 4);
+            if (lds_bytes + lds_static > 160 * 1024) fused = false;
+        }
+        if (fused) {
+            const size_t a_hdr = 256, need = a_hdr + ((size_t)n_tiles * 4 + 255) / 256 * 256;
+            if (need > s->tail_cap) {
+                if (s->tail_buf) (void)hipFree(s->tail_buf);
+                s->tail_buf = nullptr;
+                s->tail_cap = 0;
+                SP_HIP(hipMalloc(&s->tail_buf, need));
+                s->tail_cap = need;
+            }
+            char*         tb = static_cast<char*>(s->tail_buf);
+            spd::TailArgs ta{};
+            ta.n_prep      = n_tiles;
+            ta.n_items     = n_tiles * cp.chunks;
+            ta.chunks      = (uint32_t)cp.chunks;
+            ta.chunk_len   = cp.len;
+            ta.gens_per_px = cp.gens;
+            ta.n_px        = n_px;
+            ta.hits        = a.hits;
+            ta.L           = a.L;
+            ta.gens        = a.gens;
+            ta.snap_ctl    = a.snap_ctl;
+            ta.draws       = a.draws;
+            ta.ready       = reinterpret_cast<uint32_t*>(tb + a_hdr);
+            SP_HIP(hipMemcpyAsync(tb, &ta, sizeof(ta), hipMemcpyHostToDevice, stream));
+            SP_HIP(hipMemsetAsync(ta.ready, 0, (size_t)n_tiles * 4, stream));
+            spd::RenderArgs ra{};
+            ra.out          = d_out;
+            ra.tile_ids     = d_ids;
+            ra.num_tiles    = n_tiles;
+            ra.tiles_x      = a.tiles_x;
+            ra.spp          = spp_u;
+            ra.integrator   = integ;
+            ra.tile_counter = s->ck_ctr;
+            ra.counters     = s->counters;
+            ra.tail_prep    = ta.n_prep;
+            ra.tail_items   = ta.n_items;
+            const int     t_per_cu = spd::tail_blocks_per_cu(4, lds_bytes);
+            const int64_t t_waves  = (int64_t)s->n_cu * t_per_cu * 4;
+            // P: the preps ahead of the first chunks; the rest are dealt one per tile's chunks
+            int64_t front = std::max<int64_t>(1, t_waves / SP_CK_FRONT_DIV);
+            if (const char* v = std::getenv("SP_CK_FRONT_DIV")) front = std::max<int64_t>(1, t_waves / std::max(1, std::atoi(v)));
+            ra.tail_front = front;
+            ra.tail       = reinterpret_cast<const spd::TailArgs*>(tb);
+            const int t_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * t_per_cu,
+                                                                               (n_tiles * (cp.chunks + 1) + 3) / 4));
+            SP_HIP(hipEventRecord(s->ev0, stream));
+            SP_HIP(spd::chunk_camera(s->dev, a, s->n_cu, stream));
+            SP_HIP(spd::launch_tail(s->dev, ra, 4, t_blocks, lds_bytes, stream));
+            SP_HIP(spd::chunk_sum(s->dev, a, stream));
+            launches = 3;
+        } else {
+            SP_HIP(hipEventRecord(s->ev0, stream));
+            SP_HIP(spd::chunk_render(s->dev, a, blocks, s->n_cu, stream));
+            launches = 4;
+        }
     } else {
         const int    rs_words  = spd::rsqrt_words(s->dev);
         const size_t lds_bytes = (size_t)rs_words * 4 + (size_t)4 * s->dev.stack_words * 64 * 4;

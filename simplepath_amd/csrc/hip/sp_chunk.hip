@@ -323,6 +323,21 @@ int chunk_blocks_per_cu(size_t lds_bytes)
     return n > 0 ? n : 1;
 }
 
+hipError_t chunk_camera(const Scene& sc, const ChunkArgs& a, int n_cu, hipStream_t stream)
+{
+    const size_t rs_bytes    = (size_t)rsqrt_words(sc) * 4;
+    const size_t stack_bytes = (size_t)WAVES_PER_BLOCK * sc.stack_words * 64 * 4;
+    const int64_t cam_waves  = a.num_tiles * (int64_t)a.spp;
+    int           cam_per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&cam_per_cu, ck_camera, 64 * WAVES_PER_BLOCK, rs_bytes + stack_bytes) !=
+            hipSuccess || cam_per_cu < 1)
+        cam_per_cu = 1;
+    const int64_t cam_blocks = std::max<int64_t>(1, std::min<int64_t>((cam_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK,
+                                                                      (int64_t)cam_per_cu * std::max(1, n_cu)));
+    hipLaunchKernelGGL(ck_camera, dim3((unsigned)cam_blocks), dim3(64 * WAVES_PER_BLOCK), rs_bytes + stack_bytes, stream, sc, a);
+    return hipGetLastError();
+}
+
 hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int n_cu, hipStream_t stream)
 {
     const size_t rs_bytes    = (size_t)rsqrt_words(sc) * 4;

@@ -30,6 +30,9 @@ struct ChunkArgs {
 
 int        chunk_blocks_per_cu(size_t lds_bytes);
 hipError_t chunk_render(const Scene& sc, const ChunkArgs& a, int persistent_blocks, int n_cu, hipStream_t stream);
+// ck_camera alone (the fused form: sp_capi.hip runs the counts and the shading in the megakernel's
+// tail kernel, sp_mega.hpp)
+hipError_t chunk_camera(const Scene& sc, const ChunkArgs& a, int n_cu, hipStream_t stream);
 // ck_sum alone: image(p) from the per-sample radiance a.L, written at the slots a.slot_map names
 hipError_t chunk_sum(const Scene& sc, const ChunkArgs& a, hipStream_t stream);
 

@@ -56,7 +56,7 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
                                           uint32_t& samples_total)
 {
     const TailArgs& ta     = *args.tail;
-    const int64_t   slot   = args.order[k];
+    const int64_t   slot   = args.order ? args.order[k] : k;
     const int32_t   tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
     const uint32_t  px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
     const uint32_t  py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
@@ -68,6 +68,26 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
     // main.cpp:73; generation 0 (the seeded state) is never drawn from: the seed writes generation 1
     if (inside) rng_seed_twisted(rng, ((px << 16u) | py) ^ 0xb0ae9d99u);
     uint32_t T = 0; // stream position (words drawn) before sample i
+    if (ta.draws) {
+        // the sample-chunk pipeline's form: counts from ck_camera, summed in batches of loads that
+        // are all in flight together (sp_chunk.hip ck_count)
+        const uint16_t* dp = ta.draws + p;
+        for (uint32_t i0 = 0; i0 < args.spp; i0 += 8) {
+            uint32_t d[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = (inside && i0 + j < args.spp) ? (uint32_t)dp[(size_t)(i0 + j) * ta.n_px] : 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t i = i0 + (uint32_t)j;
+                if (i < args.spp && i % ta.chunk_len == 0) {
+                    const uint32_t g = T ? (T - 1) / MT_N + 1 : 0u;
+                    const uint32_t w = T ? T - (g - 1) * MT_N : (uint32_t)MT_N;
+                    ta.snap_ctl[(size_t)(i / ta.chunk_len) * ta.n_px + p] = w | (g << 16);
+                }
+                T += d[j];
+            }
+        }
+    } else
     for (uint32_t i = 0; i < args.spp; ++i) {
         if (i % ta.chunk_len == 0) { // the lazy-switch form rng_skip leaves (sp_chunk.hip ck_count)
             const uint32_t g = T ? (T - 1) / MT_N + 1 : 0u;
@@ -98,8 +118,10 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
         const uint32_t G = T ? (T - 1) / MT_N + 1 : 0u;
 #pragma unroll 1
         for (uint32_t g = 1; g < G; ++g) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(rng, (int)g), mt_buf(rng, (int)g + 1));
-        if (sc.max_depth > 0) rays_total += args.spp; // the camera rays (trace() counts them)
-        samples_total += args.spp;
+        if (!ta.draws) { // (the sample-chunk pipeline counts camera rays and samples on the host)
+            if (sc.max_depth > 0) rays_total += args.spp; // the camera rays (trace() counts them)
+            samples_total += args.spp;
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -122,7 +144,7 @@ __device__ __forceinline__ void tail_chunk(const Scene& sc, const RenderArgs& ar
         while (__hip_atomic_load(ta.ready + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(4);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int64_t  slot   = args.order[k];
+    const int64_t  slot   = args.order ? args.order[k] : k;
     const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
     const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
     const uint32_t py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
@@ -204,6 +226,25 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
         const int64_t item = __shfl(grabbed, 0, 64);
         if constexpr (TAIL) {
+            if (args.tail_front > 0) { // every tile cut: preps interleaved with the chunks
+                const int64_t K = args.tail_prep, C = args.tail_items / max<int64_t>(1, K), P = min(args.tail_front, K);
+                if (item >= K + args.tail_items) break;
+                int64_t   idx  = item;
+                bool      prep = item < P;
+                if (!prep) {
+                    const int64_t j = item - P, full = K - P; // groups 0 .. full - 1: C chunks + prep g + P
+                    if (j < full * (C + 1)) {
+                        const int64_t g = j / (C + 1), r = j % (C + 1);
+                        prep            = r == C;
+                        idx             = prep ? g + P : g * C + r;
+                    } else {
+                        idx = full * C + (j - full * (C + 1)); // the last P tiles' chunks
+                    }
+                }
+                if (prep) tail_prep(sc, args, q, st, idx, (uint32_t)lane, dx, dy, rays_total, samples_total);
+                else tail_chunk(sc, args, q, st, idx, (uint32_t)lane, dx, dy, rays_total, shadow_total, draws_total);
+                continue;
+            }
             if (item >= args.num_tiles + args.tail_items) break;
             if (item < args.tail_prep) {
                 tail_prep(sc, args, q, st, item, (uint32_t)lane, dx, dy, rays_total, samples_total);
