@@ -212,7 +212,7 @@ typedef struct sp_render_params {
                                          automatic (a one-sample probe times every tile; tiles
                                          slower than 2x the mean go first, then 24 cost classes a
                                          quarter octave apart; from 6 tiles per wave and 128 spp --
-                                         3 with tail chunks (ABI 6) --, IterativeRRNEE from 4 tiles
+                                         2.5 with tail chunks (ABI 6) --, IterativeRRNEE from 4 tiles
                                          per wave and 16 spp);
                                          > 0: with this factor whenever it can apply; < 0: queue
                                          order.  It cannot apply, and the frame renders in queue
@@ -235,9 +235,9 @@ typedef struct sp_render_params {
                                          order are rendered as sample chunks at the end of the
                                          persistent queue, so the frame ends on short work items
                                          (identical image and counts).  0 = automatic: where it
-                                         applies, waves / n_tiles clamped to [0.12, 0.3] (and AUTO
-                                         then picks the megakernel from 3 tiles per persistent wave
-                                         and 128 spp, a 2-GPU shard of a 1080p frame included);
+                                         applies, waves / n_tiles clamped to [0.12, 0.4] (and AUTO
+                                         then picks the megakernel from 2.5 tiles per persistent
+                                         wave and 128 spp: the 2- and 3-GPU shards of a 1080p frame);
                                          < 0 off, else (0, 1].                                      */
     int32_t        reserved;          /* must be 0                                                  */
 } sp_render_params;

@@ -954,7 +954,7 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
 #define SP_CK_FUSED 1
 #endif
 #ifndef SP_CK_FRONT_DIV
-#define SP_CK_FRONT_DIV 16
+#define SP_CK_FRONT_DIV 8
 #endif
 
 // Sample-chunk buffer plan (sp_chunk.hip): the same sizes decide AUTO and are allocated.
@@ -1125,14 +1125,15 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     const double ck_budget = std::min(ck_max_gb * 1e9, (double)free_b + (double)s->ck_cap);
     bool image_light = false;
     for (const auto& l : s->host->lights) image_light = image_light || l.kind == SP_LIGHT_IMAGE_ENVIRONMENT;
-    // Megakernel tail chunks (below): DirectLighting from 3 tiles per persistent wave (16 per CU at
-    // full occupancy) and 128 spp, where the draw counts are known from the camera hits.  There the
-    // megakernel with its tile order and tail chunks beats the sample chunks (bunny 2-way shard
-    // 16200 tiles: 3620-3640 against 3170 Mrays/s; lucy 2-way 3227 against 2885; 4-way, 2 tiles
-    // per wave: 2820-2980 against 3103 -- profiles/r06/tail/ab_shards*.log), so AUTO takes it.
+    // Megakernel tail chunks (below): DirectLighting from 2.5 tiles per persistent wave (16 per CU
+    // at full occupancy) and 128 spp, where the draw counts are known from the camera hits.  There
+    // the megakernel with its tile order and tail chunks beats the sample chunks (bunny 2-way shard
+    // 16200 tiles: 3620-3640 against 3170 Mrays/s, lucy 2-way 3227 against 2885; 3-way, 2.6 tiles
+    // per wave: 3398-3412 at a fraction of 0.4 against the fused chunks' 3321-3344; 4-way, 2 per
+    // wave: 2820-2980 against 3297 -- profiles/r06/tail/ab_shards*.log, ab_fused*.log).
     const int64_t tail_waves = (int64_t)std::max(1, s->n_cu) * 16;
     const bool    tail_auto  = integ == SP_INTEGRATOR_DIRECT_LIGHTING && !image_light && s->dev.n_lights <= 1000 &&
-                           spp_u >= 128 && n_tiles >= 3 * tail_waves && p->tail_fraction >= 0.0f;
+                           spp_u >= 128 && 2 * n_tiles >= 5 * tail_waves && p->tail_fraction >= 0.0f;
     if (pipeline == SP_PIPELINE_AUTO) {
         if (wave_ok && n_tiles >= wave_min) pipeline = SP_PIPELINE_WAVEFRONT;
         else if (tail_auto) pipeline = SP_PIPELINE_MEGAKERNEL;
@@ -1465,8 +1466,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // order.  sp_render_params.tile_order_factor > 0 forces it with that factor, < 0 turns it off.
         const bool rrnee = integ == SP_INTEGRATOR_ITERATIVE_RRNEE;
         // (DirectLighting with tail chunks: from 3 tiles per wave, tail_auto above)
-        const int64_t tpw   = rrnee ? 4 : (tail_auto ? 3 : 6);
-        float         hoist = (n_tiles >= tpw * (int64_t)waves && p->samples_per_pixel >= (rrnee ? 16u : 128u)) ? 2.0f : 0.0f;
+        const int64_t tpw2  = rrnee ? 8 : (tail_auto ? 5 : 12); // tiles per wave x 2
+        float         hoist = (2 * n_tiles >= tpw2 * (int64_t)waves && p->samples_per_pixel >= (rrnee ? 16u : 128u)) ? 2.0f : 0.0f;
         if (p->tile_order_factor != 0.0f) hoist = std::max(0.0f, p->tile_order_factor);
         if (hoist > 0.0f && n_tiles > (int64_t)waves && spd::has_probe(integ)) {
             if ((size_t)n_tiles > s->order_cap) {
@@ -1504,9 +1505,9 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             // automatic: SP_TAIL_FRAC, or the environment's SP_TAIL_FRAC (A/B runs); the caller's
             // tail_fraction when set (< 0: off)
             // automatic: one tile per persistent wave's worth (waves / n_tiles: 0.126 for the 1-GPU
-            // 1080p frame, 0.25 for a 2-way shard), within [SP_TAIL_FRAC, 0.3] -- measured best
-            // 0.12-0.16 and 0.2-0.3 there (profiles/r06/tail/)
-            float tail_frac = std::min(0.3f, std::max(SP_TAIL_FRAC, (float)((double)waves / (double)n_tiles)));
+            // 1080p frame, 0.25 for a 2-way shard, 0.38 for a 3-way one), within [SP_TAIL_FRAC, 0.4]
+            // -- measured best 0.12-0.16, 0.2-0.3 and 0.4 there (profiles/r06/tail/)
+            float tail_frac = std::min(0.4f, std::max(SP_TAIL_FRAC, (float)((double)waves / (double)n_tiles)));
             tail_ch         = SP_TAIL_CHUNKS;
             if (const char* v = std::getenv("SP_TAIL_FRAC")) tail_frac = (float)std::atof(v);
             if (const char* v = std::getenv("SP_TAIL_CHUNKS")) tail_ch = std::atoi(v);

@@ -523,13 +523,18 @@ static __shared__ uint32_t rho_rng_sink[64];
 #ifndef SP_RNG_PAIR
 #define SP_RNG_PAIR 0
 #endif
-template <bool NT = false>
+// PAIR: the pair form for this call (default SP_RNG_PAIR; IterativeRRNEE's served estimates choose
+// their own, SP_SERVED_PAIR).
+#ifndef SP_SERVED_PAIR
+#define SP_SERVED_PAIR SP_RNG_PAIR
+#endif
+template <bool NT = false, bool PAIR = (SP_RNG_PAIR != 0)>
 __device__ __forceinline__ void rng_raw2(Rng& r, uint64_t& w0, uint64_t& w1)
 {
     // pairs need even lane blocks: with MT_BLK % 2 != 0 (e.g. 3) words 2j, 2j + 1 can sit in two
     // blocks and a lane's block is not 16-byte aligned
-    static_assert(!SP_RNG_PAIR || MT_BLK == 1 || MT_BLK % 2 == 0, "SP_RNG_PAIR needs an even MT_BLK");
-    if constexpr (SP_RNG_PAIR && MT_BLK >= 2 && MT_BLK % 2 == 0 && RNG_PF == 0) {
+    static_assert(!PAIR || MT_BLK == 1 || MT_BLK % 2 == 0, "SP_RNG_PAIR needs an even MT_BLK");
+    if constexpr (PAIR && MT_BLK >= 2 && MT_BLK % 2 == 0 && RNG_PF == 0) {
         if (r.idx >= MT_N) { // the buffer switch of rng_raw
             if (!NT && !r.ready) {
                 SP_TD(td_twist(TD_TWIST));
@@ -2135,7 +2140,7 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     return s;
 }
 // mf_sample with the precomputed wo terms (draw order: U2, then U1)
-template <bool NT = false>
+template <bool NT = false, bool PAIR = (SP_RNG_PAIR != 0)>
 __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPre& p, f3 wo, Rng& rng, const Rsq& q)
 {
     MSample r;
@@ -2145,7 +2150,7 @@ __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPr
     r.props = 0;
     if (wo.y == 0.0f) return r;
     uint64_t u2, u1;
-    rng_raw2<NT>(rng, u2, u1); // U2 first, then U1
+    rng_raw2<NT, PAIR>(rng, u2, u1); // U2 first, then U1
     const float U2 = canonical_from_u64(u2);
     const float U1 = canonical_from_u64(u1);
     P2          sl = beckmann_sample11_pre(p, U1, U2);
@@ -2185,6 +2190,7 @@ __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPr
     r.props = PROP_GLOSSY | PROP_REFLECTIVE;
     return r;
 }
+template <bool PAIR = (SP_RNG_PAIR != 0)>
 __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
     const BeckPre p = beck_pre(m, wo, q);
@@ -2194,7 +2200,7 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
     rng_touch(rng, 32, (__attribute__((address_space(3))) void*)rho_rng_sink);
 #endif
     for (unsigned i = 0; i < 16u; ++i) {
-        const MSample s = mf_sample_pre<true>(m, p, wo, rng, q);
+        const MSample s = mf_sample_pre<true, PAIR>(m, p, wo, rng, q);
         if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
     }
     return cdivs(r, (float)16u);
@@ -2238,6 +2244,7 @@ __device__ __forceinline__ uint8_t* srv_req_of(int wave) { return reinterpret_ca
 #endif
 
 // OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
+template <bool PAIR = (SP_RNG_PAIR != 0)>
 __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
 {
 #if SP_SERVE_RHO
@@ -2258,7 +2265,7 @@ __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rn
     }
 #endif
     rgb r0;
-    SP_WPROF(1, r0 = mf_rho16(m, wo, rng, q));
+    SP_WPROF(1, r0 = mf_rho16<PAIR>(m, wo, rng, q));
     const rgb r1 = cscale(m.lambert_albedo, k_pi); // LambertianBRDF::rho_impl
     float     sum = 0.0f;
     w[0] = luminance(r0);
@@ -2881,7 +2888,7 @@ __device__ __forceinline__ void served_weights(const Material& m, f3 wo, uint64_
     sr.ready = 1;
     sr.draws = 0;
     if (SP_XP_SERVED_FREE) sr.lin = 2;
-    glossy_weights(m, wo, sr, q, w);
+    glossy_weights<(SP_SERVED_PAIR != 0)>(m, wo, sr, q, w);
 }
 // want: this lane's eval / pdf / sample estimates of the light being estimated (k = 0, 1, 2);
 // want_a: its deferred Material::sample of the bounce (k = 3, at c.rng.srv_pwA).  All lanes call.
