@@ -16,6 +16,14 @@
 #ifndef SP_SERVE_SAMPLE
 #define SP_SERVE_SAMPLE 1
 #endif
+// Served estimates read their owner's 32 words as one aligned 16-byte pair per sample whatever the
+// parity (sp_path.hpp SP_RHO_ALIGNED): elf 1024^2 @ 16 spp 1067-1084 -> 1085-1098, its 8-way shard
+// 1236-1243 -> 1253-1270 Mrays/s (profiles/r06/served/ab_aligned.log); the lanes' own estimates
+// aligned too measured lower (1080-1092, 1250-1254), and paired draws with a single-load branch
+// for odd positions lost (SP_SERVED_PAIR: 1039-1051, 1196-1199).
+#ifndef SP_SERVED_ALIGNED
+#define SP_SERVED_ALIGNED 1
+#endif
 #include "sp_mega.hpp"
 
 namespace spd {

@@ -528,6 +528,9 @@ static __shared__ uint32_t rho_rng_sink[64];
 #ifndef SP_SERVED_PAIR
 #define SP_SERVED_PAIR SP_RNG_PAIR
 #endif
+#ifndef SP_SERVED_ALIGNED
+#define SP_SERVED_ALIGNED SP_RHO_ALIGNED
+#endif
 template <bool NT = false, bool PAIR = (SP_RNG_PAIR != 0)>
 __device__ __forceinline__ void rng_raw2(Rng& r, uint64_t& w0, uint64_t& w1)
 {
@@ -2139,6 +2142,8 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     s.y = erfinv(2.0f * std_max(U2, 1e-6f) - 1.0f);
     return s;
 }
+__device__ __forceinline__ MSample mf_sample_pre_u(const Material& m, const BeckPre& p, f3 wo, uint64_t u2, uint64_t u1,
+                                                   const Rsq& q);
 // mf_sample with the precomputed wo terms (draw order: U2, then U1)
 template <bool NT = false, bool PAIR = (SP_RNG_PAIR != 0)>
 __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPre& p, f3 wo, Rng& rng, const Rsq& q)
@@ -2151,6 +2156,17 @@ __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPr
     if (wo.y == 0.0f) return r;
     uint64_t u2, u1;
     rng_raw2<NT, PAIR>(rng, u2, u1); // U2 first, then U1
+    return mf_sample_pre_u(m, p, wo, u2, u1, q);
+}
+// mf_sample_pre from its two drawn (tempered) words
+__device__ __forceinline__ MSample mf_sample_pre_u(const Material& m, const BeckPre& p, f3 wo, uint64_t u2, uint64_t u1,
+                                                   const Rsq& q)
+{
+    MSample r;
+    r.color = mkc(0, 0, 0);
+    r.dir   = mk(0, 0, 0);
+    r.pdf   = 0.0f;
+    r.props = 0;
     const float U2 = canonical_from_u64(u2);
     const float U1 = canonical_from_u64(u1);
     P2          sl = beckmann_sample11_pre(p, U1, U2);
@@ -2190,7 +2206,16 @@ __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPr
     r.props = PROP_GLOSSY | PROP_REFLECTIVE;
     return r;
 }
-template <bool PAIR = (SP_RNG_PAIR != 0)>
+// SP_RHO_ALIGNED: the estimate's 32 words (idx .. idx + 31, reserved: no twist) are read as one
+// aligned 16-byte pair per sample, whatever the parity of idx: at an odd idx a sample's two words
+// are the high word of one pair (carried from the previous load) and the low word of the next, so
+// every lane runs the same code -- no branch between pair and single loads (rng_raw2), 16 loads
+// per estimate.  Same words in the same order; the stream then skips the 32 words (the state 32
+// draws leave).  Needs even lane blocks and no draw-ahead window.
+#ifndef SP_RHO_ALIGNED
+#define SP_RHO_ALIGNED 0
+#endif
+template <bool PAIR = (SP_RNG_PAIR != 0), bool ALIGN = (SP_RHO_ALIGNED != 0)>
 __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
     const BeckPre p = beck_pre(m, wo, q);
@@ -2199,6 +2224,25 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
 #if SP_RHO_TOUCH
     rng_touch(rng, 32, (__attribute__((address_space(3))) void*)rho_rng_sink);
 #endif
+    if constexpr (ALIGN && MT_BLK % 2 == 0 && RNG_PF == 0 && !SP_XP_SERVED_FREE) {
+        if (wo.y == 0.0f) return cdivs(r, (float)16u); // mf_sample draws nothing: every sample is black
+        const int       odd   = rng.idx & 1;
+        const uint64_t* cur   = mt_buf(rng, rng.cur);
+        const uint64_t* next  = mt_buf(rng, mt_next(rng));
+        uint64_t        carry = odd ? cur[mt_off(rng.idx)] : 0ull;
+        for (unsigned i = 0; i < 16u; ++i) {
+            const int       t = rng.idx + odd + 2 * (int)i; // even: a whole aligned pair
+            const uint64_t* b = (t < MT_N) ? cur + mt_off(t) : next + mt_off(t - MT_N);
+            SP_TD(td_lines(rng.td_cat, b, 16));
+            const ulonglong2 w  = *reinterpret_cast<const ulonglong2*>(b);
+            const uint64_t   w0 = odd ? carry : w.x, w1 = odd ? w.x : w.y;
+            carry               = w.y;
+            const MSample s     = mf_sample_pre_u(m, p, wo, mt_temper(w0), mt_temper(w1), q);
+            if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
+        }
+        rng_skip_reserved(rng, 32);
+        return cdivs(r, (float)16u);
+    }
     for (unsigned i = 0; i < 16u; ++i) {
         const MSample s = mf_sample_pre<true, PAIR>(m, p, wo, rng, q);
         if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
@@ -2244,7 +2288,7 @@ __device__ __forceinline__ uint8_t* srv_req_of(int wave) { return reinterpret_ca
 #endif
 
 // OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
-template <bool PAIR = (SP_RNG_PAIR != 0)>
+template <bool PAIR = (SP_RNG_PAIR != 0), bool ALIGN = (SP_RHO_ALIGNED != 0)>
 __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
 {
 #if SP_SERVE_RHO
@@ -2265,7 +2309,7 @@ __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rn
     }
 #endif
     rgb r0;
-    SP_WPROF(1, r0 = mf_rho16<PAIR>(m, wo, rng, q));
+    SP_WPROF(1, r0 = (mf_rho16<PAIR, ALIGN>(m, wo, rng, q)));
     const rgb r1 = cscale(m.lambert_albedo, k_pi); // LambertianBRDF::rho_impl
     float     sum = 0.0f;
     w[0] = luminance(r0);
@@ -2888,7 +2932,7 @@ __device__ __forceinline__ void served_weights(const Material& m, f3 wo, uint64_
     sr.ready = 1;
     sr.draws = 0;
     if (SP_XP_SERVED_FREE) sr.lin = 2;
-    glossy_weights<(SP_SERVED_PAIR != 0)>(m, wo, sr, q, w);
+    glossy_weights<(SP_SERVED_PAIR != 0), (SP_SERVED_ALIGNED != 0)>(m, wo, sr, q, w);
 }
 // want: this lane's eval / pdf / sample estimates of the light being estimated (k = 0, 1, 2);
 // want_a: its deferred Material::sample of the bounce (k = 3, at c.rng.srv_pwA).  All lanes call.
