@@ -531,6 +531,9 @@ static __shared__ uint32_t rho_rng_sink[64];
 #ifndef SP_SERVED_ALIGNED
 #define SP_SERVED_ALIGNED SP_RHO_ALIGNED
 #endif
+#ifndef SP_SERVED_TOUCH
+#define SP_SERVED_TOUCH SP_RHO_TOUCH
+#endif
 template <bool NT = false, bool PAIR = (SP_RNG_PAIR != 0)>
 __device__ __forceinline__ void rng_raw2(Rng& r, uint64_t& w0, uint64_t& w1)
 {
@@ -2215,14 +2218,14 @@ __device__ __forceinline__ MSample mf_sample_pre_u(const Material& m, const Beck
 #ifndef SP_RHO_ALIGNED
 #define SP_RHO_ALIGNED 0
 #endif
-template <bool PAIR = (SP_RNG_PAIR != 0), bool ALIGN = (SP_RHO_ALIGNED != 0)>
+template <bool PAIR = (SP_RNG_PAIR != 0), bool ALIGN = (SP_RHO_ALIGNED != 0), bool TOUCH = (SP_RHO_TOUCH != 0)>
 __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
     const BeckPre p = beck_pre(m, wo, q);
     rgb           r = mkc(0, 0, 0);
     rng_reserve(rng, 32); // the loop below draws at most 32 words and never twists
 #if SP_RHO_TOUCH
-    rng_touch(rng, 32, (__attribute__((address_space(3))) void*)rho_rng_sink);
+    if constexpr (TOUCH) rng_touch(rng, 32, (__attribute__((address_space(3))) void*)rho_rng_sink);
 #endif
     if constexpr (ALIGN && MT_BLK % 2 == 0 && RNG_PF == 0 && !SP_XP_SERVED_FREE) {
         if (wo.y == 0.0f) return cdivs(r, (float)16u); // mf_sample draws nothing: every sample is black
@@ -2288,7 +2291,7 @@ __device__ __forceinline__ uint8_t* srv_req_of(int wave) { return reinterpret_ca
 #endif
 
 // OneSampleMaterial::get_selection_weights for the glossy pair {microfacet, lambertian}
-template <bool PAIR = (SP_RNG_PAIR != 0), bool ALIGN = (SP_RHO_ALIGNED != 0)>
+template <bool PAIR = (SP_RNG_PAIR != 0), bool ALIGN = (SP_RHO_ALIGNED != 0), bool TOUCH = (SP_RHO_TOUCH != 0)>
 __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rng, const Rsq& q, float w[2])
 {
 #if SP_SERVE_RHO
@@ -2309,7 +2312,7 @@ __device__ __forceinline__ void glossy_weights(const Material& m, f3 wo, Rng& rn
     }
 #endif
     rgb r0;
-    SP_WPROF(1, r0 = (mf_rho16<PAIR, ALIGN>(m, wo, rng, q)));
+    SP_WPROF(1, r0 = (mf_rho16<PAIR, ALIGN, TOUCH>(m, wo, rng, q)));
     const rgb r1 = cscale(m.lambert_albedo, k_pi); // LambertianBRDF::rho_impl
     float     sum = 0.0f;
     w[0] = luminance(r0);
@@ -2932,7 +2935,7 @@ __device__ __forceinline__ void served_weights(const Material& m, f3 wo, uint64_
     sr.ready = 1;
     sr.draws = 0;
     if (SP_XP_SERVED_FREE) sr.lin = 2;
-    glossy_weights<(SP_SERVED_PAIR != 0), (SP_SERVED_ALIGNED != 0)>(m, wo, sr, q, w);
+    glossy_weights<(SP_SERVED_PAIR != 0), (SP_SERVED_ALIGNED != 0), (SP_SERVED_TOUCH != 0)>(m, wo, sr, q, w);
 }
 // want: this lane's eval / pdf / sample estimates of the light being estimated (k = 0, 1, 2);
 // want_a: its deferred Material::sample of the bounce (k = 3, at c.rng.srv_pwA).  All lanes call.

@@ -25,6 +25,11 @@
 #ifndef SP_SERVED_ALIGNED
 #define SP_SERVED_ALIGNED 1
 #endif
+// ... and without the LDS-DMA touch ahead of them (the owners' own estimates keep it): level on elf
+// 1024^2 @ 16 spp (1080-1092 against 1084-1085), the 8-way shard 1254-1270 -> 1275 (ab_notouch.log)
+#ifndef SP_SERVED_TOUCH
+#define SP_SERVED_TOUCH 0
+#endif
 #include "sp_mega.hpp"
 
 namespace spd {
