@@ -1363,7 +1363,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             ra.counters     = s->counters;
             ra.tail_prep    = ta.n_prep;
             ra.tail_items   = ta.n_items;
-            const int     t_per_cu = spd::tail_blocks_per_cu(4, lds_bytes);
+            const int     t_per_cu = spd::tail_blocks_per_cu(0, lds_bytes); // 0: sp_fused_kernel
             const int64_t t_waves  = (int64_t)s->n_cu * t_per_cu * 4;
             // P: the preps ahead of the first chunks; the rest are dealt one per tile's chunks
             int64_t front = std::max<int64_t>(1, t_waves / SP_CK_FRONT_DIV);
@@ -1374,7 +1374,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                                                                                (n_tiles * (cp.chunks + 1) + 3) / 4));
             SP_HIP(hipEventRecord(s->ev0, stream));
             SP_HIP(spd::chunk_camera(s->dev, a, s->n_cu, stream));
-            SP_HIP(spd::launch_tail(s->dev, ra, 4, t_blocks, lds_bytes, stream));
+            SP_HIP(spd::launch_tail(s->dev, ra, 0, t_blocks, lds_bytes, stream));
             SP_HIP(spd::chunk_sum(s->dev, a, stream));
             launches = 3;
         } else {

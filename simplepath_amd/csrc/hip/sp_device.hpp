@@ -184,7 +184,7 @@ struct TailArgs {
     uint64_t* gens;        // [K][gens_per_px] generation buffers (mt_off layout), generation g in buffer g
     uint32_t* snap_ctl;    // [chunks][n_px] stream position at each chunk start: idx | gen << 16
     uint32_t* ready;       // [K] 1 once tile k's prep item has published its store (zeroed per render)
-    // The sample-chunk pipeline's form (sp_chunk.hip, RenderArgs::tail_front > 0): ck_camera has
+    // The sample-chunk pipeline's fused form (sp_fused_kernel, sp_capi.hip): ck_camera has
     // stored the hit records, light-only radiance and each sample's draw count, so a prep item only
     // turns the counts into chunk starts and twists the store; every tile is cut (K = num_tiles, no
     // whole tiles), and the preps run interleaved with the chunks (tail_front).
@@ -209,9 +209,10 @@ struct RenderArgs {
     // sp_tail_kernel only: the queue's prep and chunk item counts, and the rest of TailArgs in
     // device memory (read per item: kernel arguments held across the persistent loop cost SGPRs)
     int64_t         tail_prep, tail_items;
-    // 0: queue [prep 0..K) [whole tiles K..num_tiles) [chunks]; > 0 (all tiles cut, K = num_tiles):
-    // [prep 0..P) then per tile g its chunks followed by prep g + P, P = tail_front -- the memory-bound
-    // preps run beside the compute-bound chunks, each P tiles ahead of its own chunks
+    // sp_tail_kernel: queue [prep 0..K) [whole tiles K..num_tiles) [chunks]; sp_fused_kernel (all
+    // tiles cut, K = num_tiles): [prep 0..P) then per tile g its chunks followed by prep g + P,
+    // P = tail_front -- the memory-bound preps run beside the compute-bound chunks, each P tiles
+    // ahead of its own chunks
     int64_t         tail_front;
     const TailArgs* tail;
 };

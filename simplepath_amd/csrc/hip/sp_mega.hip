@@ -168,15 +168,17 @@ size_t render_static_lds(int integ, int variant)
     return fa.sharedSizeBytes;
 }
 
+// variant 0: the sample chunks' fused form (sp_fused_kernel), else the tail kernel at 3 / 4 waves
+static KernelFn tail_kernel(int variant) { return variant == 0 ? fused_chunks() : tail_direct(variant); }
 hipError_t launch_tail(const Scene& sc, const RenderArgs& args, int variant, int blocks, size_t lds_bytes, hipStream_t stream)
 {
-    hipLaunchKernelGGL(tail_direct(variant), dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);
+    hipLaunchKernelGGL(tail_kernel(variant), dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);
     return hipGetLastError();
 }
 int tail_blocks_per_cu(int variant, size_t lds_bytes)
 {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tail_direct(variant), 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tail_kernel(variant), 64 * WAVES_PER_BLOCK, lds_bytes) != hipSuccess) return 1;
     return n > 0 ? n : 1;
 }
 

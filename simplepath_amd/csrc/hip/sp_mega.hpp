@@ -51,6 +51,8 @@ __device__ __forceinline__ Ray tail_camera_ray(const Scene& sc, uint32_t px, uin
 // then every generation of each pixel's stream, twisted once, into the store (sp_chunk.hip ck_camera
 // + ck_count in one item).  Publishes the store with an agent-scope release before setting
 // ready[k] (MI355X guide: stores, vmcnt(0), release, vmcnt(0), flag).
+// DRAWS: the sample-chunk pipeline's fused form (TailArgs::draws from ck_camera, no camera rays here).
+template <bool DRAWS>
 __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& args, const Rsq& q, Stack& st, int64_t k,
                                           uint32_t lane, uint32_t dx, uint32_t dy, uint32_t& rays_total,
                                           uint32_t& samples_total)
@@ -68,7 +70,7 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
     // main.cpp:73; generation 0 (the seeded state) is never drawn from: the seed writes generation 1
     if (inside) rng_seed_twisted(rng, ((px << 16u) | py) ^ 0xb0ae9d99u);
     uint32_t T = 0; // stream position (words drawn) before sample i
-    if (ta.draws) {
+    if constexpr (DRAWS) {
         // the sample-chunk pipeline's form: counts from ck_camera, summed in batches of loads that
         // are all in flight together (sp_chunk.hip ck_count)
         const uint16_t* dp = ta.draws + p;
@@ -87,7 +89,7 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
                 T += d[j];
             }
         }
-    } else
+    } else {
     for (uint32_t i = 0; i < args.spp; ++i) {
         if (i % ta.chunk_len == 0) { // the lazy-switch form rng_skip leaves (sp_chunk.hip ck_count)
             const uint32_t g = T ? (T - 1) / MT_N + 1 : 0u;
@@ -114,11 +116,12 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
         ta.L[((size_t)i * 3 + 2) * ta.n_px + p] = L.b;
         T += nd;
     }
+    }
     if (inside) {
         const uint32_t G = T ? (T - 1) / MT_N + 1 : 0u;
 #pragma unroll 1
         for (uint32_t g = 1; g < G; ++g) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(rng, (int)g), mt_buf(rng, (int)g + 1));
-        if (!ta.draws) { // (the sample-chunk pipeline counts camera rays and samples on the host)
+        if constexpr (!DRAWS) { // (the sample-chunk pipeline counts camera rays and samples on the host)
             if (sc.max_depth > 0) rays_total += args.spp; // the camera rays (trace() counts them)
             samples_total += args.spp;
         }
@@ -189,8 +192,10 @@ __device__ __forceinline__ void tail_chunk(const Scene& sc, const RenderArgs& ar
 // PROBE: the tile-order probe pass (sp_mega.hip) -- the same code writing each tile's wave time
 // to args.tile_time instead of radiance, compiled as its own kernel (sp_probe_kernel) so that
 // profiles list the probe and the render apart.
-// TAIL: the DirectLighting render with tail chunks (sp_tail_kernel; queue layout in TailArgs).
-template <int INTEG, bool PROBE, bool TAIL = false>
+// TAIL: 1 the DirectLighting render with tail chunks (sp_tail_kernel; queue layout in TailArgs),
+// 2 the sample-chunk pipeline's fused form (preps from ck_camera's counts interleaved with the chunks,
+// no whole tiles: sp_fused_kernel).  One kernel per form, so each carries only its own code.
+template <int INTEG, bool PROBE, int TAIL = 0>
 __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderArgs& args)
 {
     extern __shared__ uint32_t lds[];
@@ -225,8 +230,8 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
         int grabbed = 0;
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
         const int64_t item = __shfl(grabbed, 0, 64);
-        if constexpr (TAIL) {
-            if (args.tail_front > 0) { // every tile cut: preps interleaved with the chunks
+        if constexpr (TAIL == 2) {
+            { // every tile cut: preps interleaved with the chunks
                 const int64_t K = args.tail_prep, C = args.tail_items / max<int64_t>(1, K), P = min(args.tail_front, K);
                 if (item >= K + args.tail_items) break;
                 int64_t   idx  = item;
@@ -241,13 +246,14 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
                         idx = full * C + (j - full * (C + 1)); // the last P tiles' chunks
                     }
                 }
-                if (prep) tail_prep(sc, args, q, st, idx, (uint32_t)lane, dx, dy, rays_total, samples_total);
+                if (prep) tail_prep<true>(sc, args, q, st, idx, (uint32_t)lane, dx, dy, rays_total, samples_total);
                 else tail_chunk(sc, args, q, st, idx, (uint32_t)lane, dx, dy, rays_total, shadow_total, draws_total);
                 continue;
             }
+        } else if constexpr (TAIL == 1) {
             if (item >= args.num_tiles + args.tail_items) break;
             if (item < args.tail_prep) {
-                tail_prep(sc, args, q, st, item, (uint32_t)lane, dx, dy, rays_total, samples_total);
+                tail_prep<false>(sc, args, q, st, item, (uint32_t)lane, dx, dy, rays_total, samples_total);
                 continue;
             }
             if (item >= args.num_tiles) {
@@ -352,7 +358,12 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_probe_kernel(Sc
 template <int MINW>
 __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_tail_kernel(Scene sc, RenderArgs args)
 {
-    render_tiles_body<SP_INTEGRATOR_DIRECT_LIGHTING, false, true>(sc, args);
+    render_tiles_body<SP_INTEGRATOR_DIRECT_LIGHTING, false, 1>(sc, args);
+}
+template <int MINW>
+__global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_fused_kernel(Scene sc, RenderArgs args)
+{
+    render_tiles_body<SP_INTEGRATOR_DIRECT_LIGHTING, false, 2>(sc, args);
 }
 } // inline namespace SPD_LAYOUT_NS
 
@@ -365,6 +376,7 @@ KernelFn mega_mandelbrot();
 KernelFn probe_direct(int variant); // nullptr: no probe kernel (queue order)
 KernelFn probe_rrnee(int waves);
 KernelFn tail_direct(int variant); // DirectLighting with tail chunks, 3 or 4 waves per SIMD (sp_mega_tail.hip)
+KernelFn fused_chunks();           // the sample chunks' fused form, 4 waves per SIMD (sp_mega_tail.hip)
 hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
                              hipStream_t stream);
 

@@ -14,4 +14,5 @@
 
 namespace spd {
 KernelFn tail_direct(int variant) { return variant == 3 ? sp_tail_kernel<3> : sp_tail_kernel<4>; }
+KernelFn fused_chunks() { return sp_fused_kernel<4>; }
 } // namespace spd
