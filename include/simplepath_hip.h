@@ -228,16 +228,16 @@ typedef struct sp_render_params {
                                          the tile columns); any other list uses each tile's own
                                          probe time.                                                  */
     /* ---- ABI 6 ---- */
-    float          tail_fraction;     /* megakernel tail chunks (DirectLighting at 3 or 4 waves per SIMD,
-                                         with the tile order and draw counts known from the camera
-                                         hits -- no image light):
+    float          tail_fraction;     /* megakernel tail chunks (DirectLighting at 4 waves per SIMD, or
+                                         3 without an image light, with the tile order):
                                          the most expensive tail_fraction x n_tiles tiles of the
                                          order are rendered as sample chunks at the end of the
                                          persistent queue, so the frame ends on short work items
                                          (identical image and counts).  0 = automatic: where it
                                          applies, waves / n_tiles clamped to [0.12, 0.4] (and AUTO
-                                         then picks the megakernel from 2.5 tiles per persistent
-                                         wave and 128 spp: the 2- and 3-GPU shards of a 1080p frame);
+                                         then picks the megakernel with the order from 2.5 tiles per
+                                         persistent wave and 128 spp -- the 2- and 3-GPU shards of a
+                                         1080p frame -- or 4 tiles per wave and 64 spp);
                                          < 0 off, else (0, 1].                                      */
     int32_t        reserved;          /* must be 0                                                  */
 } sp_render_params;

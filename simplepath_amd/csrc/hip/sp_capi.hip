@@ -1131,9 +1131,12 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
     // 16200 tiles: 3620-3640 against 3170 Mrays/s, lucy 2-way 3227 against 2885; 3-way, 2.6 tiles
     // per wave: 3398-3412 at a fraction of 0.4 against the fused chunks' 3321-3344; 4-way, 2 per
     // wave: 2820-2980 against 3297 -- profiles/r06/tail/ab_shards*.log, ab_fused*.log).
+    // With an image light the preps replay Light::sample (TailArgs::replay): material_spheres with its
+    // image light, 1024^2 @ 64 spp (4 tiles per wave), 3814-3826 -> 3890-3895 Mrays/s (ab_spheres.log),
+    // so from 64 spp at 4 tiles per wave as well.
     const int64_t tail_waves = (int64_t)std::max(1, s->n_cu) * 16;
-    const bool    tail_auto  = integ == SP_INTEGRATOR_DIRECT_LIGHTING && !image_light && s->dev.n_lights <= 1000 &&
-                           spp_u >= 128 && 2 * n_tiles >= 5 * tail_waves && p->tail_fraction >= 0.0f;
+    const bool    tail_auto  = integ == SP_INTEGRATOR_DIRECT_LIGHTING && s->dev.n_lights <= 1000 && p->tail_fraction >= 0.0f &&
+                           ((spp_u >= 128 && 2 * n_tiles >= 5 * tail_waves) || (spp_u >= 64 && n_tiles >= 4 * tail_waves));
     if (pipeline == SP_PIPELINE_AUTO) {
         if (wave_ok && n_tiles >= wave_min) pipeline = SP_PIPELINE_WAVEFRONT;
         else if (tail_auto) pipeline = SP_PIPELINE_MEGAKERNEL;
@@ -1466,8 +1469,8 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         // order.  sp_render_params.tile_order_factor > 0 forces it with that factor, < 0 turns it off.
         const bool rrnee = integ == SP_INTEGRATOR_ITERATIVE_RRNEE;
         // (DirectLighting with tail chunks: from 3 tiles per wave, tail_auto above)
-        const int64_t tpw2  = rrnee ? 8 : (tail_auto ? 5 : 12); // tiles per wave x 2
-        float         hoist = (2 * n_tiles >= tpw2 * (int64_t)waves && p->samples_per_pixel >= (rrnee ? 16u : 128u)) ? 2.0f : 0.0f;
+        float hoist = (n_tiles >= (rrnee ? 4 : 6) * (int64_t)waves && p->samples_per_pixel >= (rrnee ? 16u : 128u)) ? 2.0f : 0.0f;
+        if (tail_auto && 2 * n_tiles >= 5 * (int64_t)waves) hoist = 2.0f; // the tail chunks need the order
         if (p->tile_order_factor != 0.0f) hoist = std::max(0.0f, p->tile_order_factor);
         if (hoist > 0.0f && n_tiles > (int64_t)waves && spd::has_probe(integ)) {
             if ((size_t)n_tiles > s->order_cap) {
@@ -1498,10 +1501,13 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
         }
         // Tail chunks (sp_mega.hpp, sp_device.hpp TailArgs): the K = tail_frac x n_tiles most
         // expensive tiles of the order are rendered as sample chunks at the end of the queue.
-        // DirectLighting at 3 or 4 waves per SIMD with the tile order and draw counts known from the
-        // camera hits (no image light); SP_TAIL_FRAC (0: off) and SP_TAIL_CHUNKS override.
+        // DirectLighting at 3 or 4 waves per SIMD with the tile order; the preps take the draw counts
+        // from the camera hits, or with an image light replay Light::sample on the stream (TailArgs
+        // replay); SP_TAIL_FRAC (0: off) and SP_TAIL_CHUNKS override.
         spd::ChunkArgs tail_sum{};
-        if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && (variant == 3 || variant == 4) && a.order) {
+        // counts replayed on the stream (an image light, or SP_CHUNK_REPLAY): the 4-wave kernel only
+        const bool tail_replay = !chunk_plan(s, 1, spp_u, 1).known_draws;
+        if (integ == SP_INTEGRATOR_DIRECT_LIGHTING && (variant == 4 || (variant == 3 && !tail_replay)) && a.order) {
             // automatic: SP_TAIL_FRAC, or the environment's SP_TAIL_FRAC (A/B runs); the caller's
             // tail_fraction when set (< 0: off)
             // automatic: one tile per persistent wave's worth (waves / n_tiles: 0.126 for the 1-GPU
@@ -1513,7 +1519,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             if (const char* v = std::getenv("SP_TAIL_CHUNKS")) tail_ch = std::atoi(v);
             if (p->tail_fraction != 0.0f) tail_frac = p->tail_fraction;
             const ChunkPlan tp = chunk_plan(s, 1, spp_u, std::max(1, tail_ch));
-            if (tail_frac > 0.0f && tp.known_draws) {
+            if (tail_frac > 0.0f) {
                 // ceil(frac x n), with frac the f32 caller value (0.05f x 5120 = 256.0000038: 256 tiles)
                 tail_k = std::min<int64_t>(n_tiles, std::max<int64_t>(1, (int64_t)std::ceil((double)tail_frac * (double)n_tiles - 1e-3)));
                 const ChunkPlan cp    = chunk_plan(s, tail_k, spp_u, std::max(1, tail_ch));
@@ -1530,6 +1536,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                 spd::TailArgs ta{};
                 tail_ch        = (int)cp.chunks;
                 ta.n_prep      = tail_k;
+                ta.replay      = tail_replay ? 1 : 0; // an image light: the preps replay Light::sample
                 ta.n_items     = tail_k * cp.chunks;
                 ta.chunks      = (uint32_t)cp.chunks;
                 ta.chunk_len   = cp.len;
@@ -1562,10 +1569,11 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             SP_HIP(hipEventRecord(s->ev_render, stream));
         }
         if (tail_k > 0) {
-            const int     t_per_cu = spd::tail_blocks_per_cu(variant, lds_bytes);
+            const int     t_var    = tail_replay ? -variant : variant; // -4: the replaying tail kernel
+            const int     t_per_cu = spd::tail_blocks_per_cu(t_var, lds_bytes);
             const int64_t t_need   = (n_tiles + a.tail_items + 3) / 4;
             const int     t_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * t_per_cu, t_need));
-            SP_HIP(spd::launch_tail(sc_run, a, variant, t_blocks, lds_bytes, stream));
+            SP_HIP(spd::launch_tail(sc_run, a, t_var, t_blocks, lds_bytes, stream));
             SP_HIP(spd::chunk_sum(sc_run, tail_sum, stream));
             launches += 1;
         } else {

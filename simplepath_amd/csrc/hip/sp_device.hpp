@@ -189,6 +189,10 @@ struct TailArgs {
     // turns the counts into chunk starts and twists the store; every tile is cut (K = num_tiles, no
     // whole tiles), and the preps run interleaved with the chunks (tail_front).
     const uint16_t* draws; // [spp][n_px] draw counts; nullptr: the prep item traces the camera rays
+    // sp_tail_kernel<4, true> (an image light): a sample's draw count depends on the drawn numbers
+    // (Light::sample's usability), so the prep item replays each sample's Light::sample draws on the
+    // stream itself (sp_chunk.hip ck_count's replay), twisting the store generation by generation
+    int32_t         replay;
 };
 
 struct RenderArgs {

@@ -168,8 +168,12 @@ size_t render_static_lds(int integ, int variant)
     return fa.sharedSizeBytes;
 }
 
-// variant 0: the sample chunks' fused form (sp_fused_kernel), else the tail kernel at 3 / 4 waves
-static KernelFn tail_kernel(int variant) { return variant == 0 ? fused_chunks() : tail_direct(variant); }
+// variant 0: the sample chunks' fused form (sp_fused_kernel), 3 / 4: the tail kernel at 3 / 4 waves,
+// -4: the tail kernel with an image light's replay (4 waves)
+static KernelFn tail_kernel(int variant)
+{
+    return variant == 0 ? fused_chunks() : tail_direct(variant < 0 ? -variant : variant, variant < 0);
+}
 hipError_t launch_tail(const Scene& sc, const RenderArgs& args, int variant, int blocks, size_t lds_bytes, hipStream_t stream)
 {
     hipLaunchKernelGGL(tail_kernel(variant), dim3(blocks), dim3(64 * WAVES_PER_BLOCK), lds_bytes, stream, sc, args);

@@ -52,7 +52,8 @@ __device__ __forceinline__ Ray tail_camera_ray(const Scene& sc, uint32_t px, uin
 // + ck_count in one item).  Publishes the store with an agent-scope release before setting
 // ready[k] (MI355X guide: stores, vmcnt(0), release, vmcnt(0), flag).
 // DRAWS: the sample-chunk pipeline's fused form (TailArgs::draws from ck_camera, no camera rays here).
-template <bool DRAWS>
+// REPLAY: an image light's counts, replayed on the stream (TailArgs::replay; sp_tail_kernel<., true>).
+template <bool DRAWS, bool REPLAY = false>
 __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& args, const Rsq& q, Stack& st, int64_t k,
                                           uint32_t lane, uint32_t dx, uint32_t dy, uint32_t& rays_total,
                                           uint32_t& samples_total)
@@ -65,8 +66,12 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
     const bool      inside = px < (uint32_t)sc.width && py < (uint32_t)sc.height;
     const size_t    p      = (size_t)k * 64 + lane;
     Rng             rng;
-    rng.lin  = 1; // generation g in buffer g of the pixel's store
-    rng.base = ta.gens + (size_t)k * ta.gens_per_px * MT_GEN_WORDS + (size_t)lane * MT_BLK;
+    rng.lin   = 1; // generation g in buffer g of the pixel's store
+    rng.base  = ta.gens + (size_t)k * ta.gens_per_px * MT_GEN_WORDS + (size_t)lane * MT_BLK;
+    rng.cur   = 0; // (a pixel outside the image keeps this state; its chunks never run)
+    rng.idx   = MT_N;
+    rng.ready = 0;
+    rng.draws = 0;
     // main.cpp:73; generation 0 (the seeded state) is never drawn from: the seed writes generation 1
     if (inside) rng_seed_twisted(rng, ((px << 16u) | py) ^ 0xb0ae9d99u);
     uint32_t T = 0; // stream position (words drawn) before sample i
@@ -90,12 +95,20 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
             }
         }
     } else {
+    constexpr bool replay = REPLAY;
     for (uint32_t i = 0; i < args.spp; ++i) {
-        if (i % ta.chunk_len == 0) { // the lazy-switch form rng_skip leaves (sp_chunk.hip ck_count)
-            const uint32_t g = T ? (T - 1) / MT_N + 1 : 0u;
-            const uint32_t w = T ? T - (g - 1) * MT_N : (uint32_t)MT_N;
-            ta.snap_ctl[(size_t)(i / ta.chunk_len) * ta.n_px + p] = w | (g << 16);
+        if (i % ta.chunk_len == 0) {
+            uint32_t snap;
+            if (replay) { // the replayed stream's own position (sp_chunk.hip ck_count)
+                snap = (uint32_t)rng.idx | ((uint32_t)rng.cur << 16);
+            } else { // the lazy-switch form rng_skip leaves (sp_chunk.hip ck_count)
+                const uint32_t g = T ? (T - 1) / MT_N + 1 : 0u;
+                const uint32_t w = T ? T - (g - 1) * MT_N : (uint32_t)MT_N;
+                snap             = w | (g << 16);
+            }
+            ta.snap_ctl[(size_t)(i / ta.chunk_len) * ta.n_px + p] = snap;
         }
+        if (replay && inside) rng_prepare(rng);
         float4   rec = make_float4(0.0f, __uint_as_float(0xffffffffu), 0.0f, 0.0f);
         rgb      L   = mkc(0, 0, 0);
         uint32_t nd  = 0;
@@ -105,7 +118,22 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
             const Hit      h   = scene_intersect(sc, ray, k_ray_epsilon, lh.hit ? lh.t : k_infinite, st);
             if (h.code != 0xffffffffu) {
                 rec = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
-                nd  = sample_draws(sc, finish_hit(sc, h, ray, q), neg(ray.d), q);
+                const Isect is = finish_hit(sc, h, ray, q);
+                if (!replay) {
+                    nd = sample_draws(sc, is, neg(ray.d), q);
+                } else { // direct_nee's draws: Light::sample, then the glossy estimate of a usable sample
+                    const f3 wo = neg(ray.d);
+                    for (int li = 0; li < sc.n_lights; ++li) {
+                        const Light   lt = uload_light(sc.lights + li);
+                        const LSample ls = light_sample(sc, lt, is.p, is.n, next2D(rng), q);
+                        if (ls.pdf == 0.0f || cblack(ls.L)) continue;
+                        const Material& m    = sc.materials[is.material];
+                        const int       base = (m.kind == SP_MAT_CLEARCOAT) ? sc.materials[m.base].kind : m.kind;
+                        if (base == SP_MAT_LAMBERTIAN) continue;
+                        const Onb o = onb_from_v(is.n, q);
+                        if (to_onb(o, wo).y != 0.0f) rng_skip(rng, 32);
+                    }
+                }
             } else if (lh.hit) {
                 L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, q)));
             }
@@ -118,6 +146,7 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
     }
     }
     if (inside) {
+        // (the replay twisted each generation as its draws reached it)
         const uint32_t G = T ? (T - 1) / MT_N + 1 : 0u;
 #pragma unroll 1
         for (uint32_t g = 1; g < G; ++g) mt_twist_blocked<SP_TWIST_SKIP_BLOCK>(mt_buf(rng, (int)g), mt_buf(rng, (int)g + 1));
@@ -192,9 +221,10 @@ __device__ __forceinline__ void tail_chunk(const Scene& sc, const RenderArgs& ar
 // PROBE: the tile-order probe pass (sp_mega.hip) -- the same code writing each tile's wave time
 // to args.tile_time instead of radiance, compiled as its own kernel (sp_probe_kernel) so that
 // profiles list the probe and the render apart.
-// TAIL: 1 the DirectLighting render with tail chunks (sp_tail_kernel; queue layout in TailArgs),
-// 2 the sample-chunk pipeline's fused form (preps from ck_camera's counts interleaved with the chunks,
-// no whole tiles: sp_fused_kernel).  One kernel per form, so each carries only its own code.
+// TAIL: 1 the DirectLighting render with tail chunks (sp_tail_kernel; queue layout in TailArgs; 3:
+// the same with an image light, its preps replaying Light::sample), 2 the sample-chunk pipeline's
+// fused form (preps from ck_camera's counts interleaved with the chunks, no whole tiles:
+// sp_fused_kernel).  One kernel per form, so each carries only its own code.
 template <int INTEG, bool PROBE, int TAIL = 0>
 __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderArgs& args)
 {
@@ -250,10 +280,10 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
                 else tail_chunk(sc, args, q, st, idx, (uint32_t)lane, dx, dy, rays_total, shadow_total, draws_total);
                 continue;
             }
-        } else if constexpr (TAIL == 1) {
+        } else if constexpr (TAIL == 1 || TAIL == 3) {
             if (item >= args.num_tiles + args.tail_items) break;
             if (item < args.tail_prep) {
-                tail_prep<false>(sc, args, q, st, item, (uint32_t)lane, dx, dy, rays_total, samples_total);
+                tail_prep<false, TAIL == 3>(sc, args, q, st, item, (uint32_t)lane, dx, dy, rays_total, samples_total);
                 continue;
             }
             if (item >= args.num_tiles) {
@@ -355,10 +385,10 @@ __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_probe_kernel(Sc
 {
     render_tiles_body<INTEG, true>(sc, args);
 }
-template <int MINW>
+template <int MINW, bool REPLAY>
 __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_tail_kernel(Scene sc, RenderArgs args)
 {
-    render_tiles_body<SP_INTEGRATOR_DIRECT_LIGHTING, false, 1>(sc, args);
+    render_tiles_body<SP_INTEGRATOR_DIRECT_LIGHTING, false, REPLAY ? 3 : 1>(sc, args);
 }
 template <int MINW>
 __global__ void __launch_bounds__(64 * WAVES_PER_BLOCK, MINW) sp_fused_kernel(Scene sc, RenderArgs args)
@@ -375,7 +405,8 @@ KernelFn mega_recursive(int integ);
 KernelFn mega_mandelbrot();
 KernelFn probe_direct(int variant); // nullptr: no probe kernel (queue order)
 KernelFn probe_rrnee(int waves);
-KernelFn tail_direct(int variant); // DirectLighting with tail chunks, 3 or 4 waves per SIMD (sp_mega_tail.hip)
+KernelFn tail_direct(int variant, bool replay); // DirectLighting with tail chunks, 3 or 4 waves per SIMD
+                                                 // (sp_mega_tail.hip; replay: an image light, 4 waves)
 KernelFn fused_chunks();           // the sample chunks' fused form, 4 waves per SIMD (sp_mega_tail.hip)
 hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
                              hipStream_t stream);

@@ -13,6 +13,10 @@
 #include "sp_mega.hpp"
 
 namespace spd {
-KernelFn tail_direct(int variant) { return variant == 3 ? sp_tail_kernel<3> : sp_tail_kernel<4>; }
+KernelFn tail_direct(int variant, bool replay)
+{
+    if (replay) return sp_tail_kernel<4, true>;
+    return variant == 3 ? sp_tail_kernel<3, false> : sp_tail_kernel<4, false>;
+}
 KernelFn fused_chunks() { return sp_fused_kernel<4>; }
 } // namespace spd

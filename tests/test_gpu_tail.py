@@ -83,14 +83,18 @@ def test_tail_chunks_match_the_oracle(scene_dir):
     assert same_bits(img, c)
 
 
-def test_no_tail_chunks_with_an_image_light(scene_dir):
+@pytest.mark.parametrize("bvh", [0, 1])
+def test_tail_chunks_with_an_image_light(scene_dir, tail_chunks, bvh):
     # with an image light a sample's draw count depends on the drawn numbers (Light::sample), so
-    # the camera pass cannot place the chunk starts: the frame renders without tail chunks
-    s = load(os.path.join(scene_dir, "material_spheres_ibl.sp"), w=640, h=512)
-    img, st = sp.render_tiles(s, "direct_lighting", 2, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=0.5)
-    assert st.tail_tiles == 0 and st.launches == 3
-    off, ost = sp.render_tiles(s, "direct_lighting", 2, pipeline="megakernel", tile_order_factor=-1.0)
-    assert same_bits(img, off) and counts(st) == counts(ost)
+    # each prep item replays Light::sample on the stream itself to place the chunk starts
+    s = load(os.path.join(scene_dir, "material_spheres_ibl.sp"), bvh=bvh, w=640, h=512)
+    off, ost = sp.render_tiles(s, "direct_lighting", 5, pipeline="megakernel", tile_order_factor=-1.0)
+    for frac, chunks in ((0.5, 2), (1.0, 5), (0.2, 64)):
+        tail_chunks(chunks)
+        img, st = sp.render_tiles(s, "direct_lighting", 5, pipeline="megakernel", tile_order_factor=2.0,
+                                  tail_fraction=frac)
+        assert st.tail_tiles > 0 and st.launches == 4
+        assert same_bits(img, off) and counts(st) == counts(ost), (frac, chunks)
 
 
 @pytest.mark.parametrize("max_depth", [0, 1])
@@ -134,3 +138,16 @@ def test_fused_sample_chunks(scene_dir, monkeypatch, front_div):
     monkeypatch.setenv("SP_CK_FUSED", "0")
     four, fst = sp.render_tiles(s, "direct_lighting", 6, ids, pipeline="chunks", chunks_per_pixel=3)
     assert fst.launches == 4 and counts(fst) == counts(rst) and same_bits(four, ref)
+
+
+def test_tail_chunks_with_replayed_counts(scene_dir, monkeypatch, tail_chunks):
+    # SP_CHUNK_REPLAY=1: the preps replay Light::sample on the stream (the image-light form,
+    # sp_tail_kernel<4, true>) for sphere lights as well -- same chunk starts, same image
+    s = load(os.path.join(scene_dir, "bunny.sp"))
+    ref, rst = sp.render_tiles(s, "direct_lighting", 6, pipeline="megakernel", tile_order_factor=-1.0)
+    monkeypatch.setenv("SP_CHUNK_REPLAY", "1")
+    for frac, chunks in ((0.3, 4), (1.0, 6)):
+        tail_chunks(chunks)
+        img, st = sp.render_tiles(s, "direct_lighting", 6, pipeline="megakernel", tile_order_factor=2.0,
+                                  tail_fraction=frac)
+        assert st.tail_tiles > 0 and counts(st) == counts(rst) and same_bits(img, ref), (frac, chunks)
