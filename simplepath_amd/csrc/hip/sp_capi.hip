@@ -1525,13 +1525,28 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
                 const ChunkPlan cp    = chunk_plan(s, tail_k, spp_u, std::max(1, tail_ch));
                 const size_t    a_hdr = 256, a_rdy = ((size_t)tail_k * 4 + 255) / 256 * 256;
                 const size_t    need  = a_hdr + a_rdy + cp.b_hits + cp.b_L + cp.b_snap + cp.b_ctl;
-                if (need > s->tail_cap) {
+                // the sample chunks' budget (chunk_max_gb, never more than the device can still give):
+                // 20 GB for bunny's 4096 tail tiles (the store: 30 generations per pixel); a scene
+                // with many lights (a store bound of 34 draws per light and sample) renders without
+                // tail chunks rather than fail
+                const double tail_budget = std::min(ck_max_gb * 1e9, (double)free_b + (double)s->tail_cap);
+                if ((double)need > tail_budget) tail_k = 0;
+                if (tail_k > 0 && need > s->tail_cap) {
                     if (s->tail_buf) (void)hipFree(s->tail_buf);
                     s->tail_buf = nullptr;
                     s->tail_cap = 0;
-                    SP_HIP(hipMalloc(&s->tail_buf, need));
-                    s->tail_cap = need;
+                    if (hipMalloc(&s->tail_buf, need) != hipSuccess) {
+                        s->tail_buf = nullptr;
+                        (void)hipGetLastError();
+                        tail_k = 0;
+                    } else {
+                        s->tail_cap = need;
+                    }
                 }
+            }
+            if (tail_k > 0) {
+                const ChunkPlan cp    = chunk_plan(s, tail_k, spp_u, std::max(1, tail_ch));
+                const size_t    a_hdr = 256, a_rdy = ((size_t)tail_k * 4 + 255) / 256 * 256;
                 char*         base = static_cast<char*>(s->tail_buf);
                 spd::TailArgs ta{};
                 tail_ch        = (int)cp.chunks;

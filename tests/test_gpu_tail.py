@@ -151,3 +151,14 @@ def test_tail_chunks_with_replayed_counts(scene_dir, monkeypatch, tail_chunks):
         img, st = sp.render_tiles(s, "direct_lighting", 6, pipeline="megakernel", tile_order_factor=2.0,
                                   tail_fraction=frac)
         assert st.tail_tiles > 0 and counts(st) == counts(rst) and same_bits(img, ref), (frac, chunks)
+
+
+def test_tail_chunks_within_the_budget(scene_dir):
+    # the tail buffers (hit records, radiance, each tail pixel's stream generations) count against
+    # chunk_max_gb like the sample chunks': over it, the frame renders without tail chunks
+    s = load(os.path.join(scene_dir, "bunny.sp"))
+    ref, rst = sp.render_tiles(s, "direct_lighting", 3, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=-1.0)
+    img, st = sp.render_tiles(s, "direct_lighting", 3, pipeline="megakernel", tile_order_factor=2.0, tail_fraction=0.5,
+                              chunk_max_gb=1e-3)
+    assert st.tail_tiles == 0 and st.launches == 3
+    assert counts(st) == counts(rst) and same_bits(img, ref)
