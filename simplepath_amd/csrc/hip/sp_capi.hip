@@ -21,7 +21,7 @@ hipError_t launch_render(const Scene& sc, const RenderArgs& args, int integ, int
                          hipStream_t stream);
 int        render_blocks_per_cu(int integ, int variant, size_t lds_bytes);
 size_t     render_static_lds(int integ, int variant);
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
+hipError_t launch_tile_order(float* tile_time, int64_t n_tiles, float factor, int tiles_x, int step, int32_t* order,
                              hipStream_t stream);
 bool       has_probe(int integ);
 hipError_t launch_probe(const Scene& sc, const RenderArgs& args, int integ, int variant, int blocks, size_t lds_bytes,
@@ -1489,12 +1489,17 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             pr.tile_time = s->d_tile_time;
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
+            // every 2nd slot timed where tail chunks follow (the others interpolated by the order kernel:
+            // bunny +0.25 %, spheres +0.8 %, lucy +0.2 %); IterativeRRNEE, whose order has no tail
+            // chunks behind it, lost 2-4 % on elf's shard with it (profiles/r06/tail/ab_probe_step.log)
+            pr.probe_step = (integ == SP_INTEGRATOR_DIRECT_LIGHTING && (tail_auto || p->tail_fraction > 0.0f)) ? 2 : 1;
+            if (const char* v = std::getenv("SP_PROBE_STEP")) pr.probe_step = std::max(1, std::atoi(v));
             SP_HIP(spd::launch_probe(sc_run, pr, integ, variant, blocks, lds_bytes, stream));
             // cost estimates blended with their queue neighbours only where those sit at known
             // image offsets: a whole frame, or a host list with a constant stride (the bench's list,
             // a rank's interleaved shard; order_neighbours); any other list keeps each tile's own time
             SP_HIP(spd::launch_tile_order(s->d_tile_time, n_tiles, hoist, order_neighbours(p, listed, n_tiles, a.tiles_x),
-                                          s->d_order, stream));
+                                          pr.probe_step, s->d_order, stream));
             SP_HIP(hipMemsetAsync(s->tile_counter, 0, sizeof(int32_t), stream));
             a.order = s->d_order;
             launches += 2;

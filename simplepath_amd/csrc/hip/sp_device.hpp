@@ -219,6 +219,7 @@ struct RenderArgs {
     // ahead of its own chunks
     int64_t         tail_front;
     const TailArgs* tail;
+    int32_t         probe_step; // sp_probe_kernel: times every probe_step-th slot (the order kernel fills the rest)
 };
 
 } // namespace spd

@@ -99,12 +99,23 @@ __device__ __forceinline__ float tile_est(const float* t, int64_t i, int64_t n, 
     const float u = t[i >= tx ? i - tx : i], d = t[i + tx < n ? i + tx : i];
     return fmaxf(row, 0.25f * (u + d) + 0.5f * t[i]);
 }
-__global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time, int64_t n, float factor, int tx, int32_t* order)
+__global__ void __launch_bounds__(1024) tile_order_kernel(float* tile_time, int64_t n, float factor, int tx, int step,
+                                                          int32_t* order)
 {
     __shared__ float s_sum[16];
     __shared__ int   s_cnt[TILE_CLASSES][16];
     __shared__ int   s_base[TILE_CLASSES];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // a probe of every step-th slot: the others from their probed queue neighbours (linear)
+    if (step > 1) {
+        for (int64_t i = tid; i < n; i += 1024) {
+            const int64_t r = i % step;
+            if (r == 0) continue;
+            const int64_t lo = i - r, hi = lo + step;
+            tile_time[i] = hi < n ? tile_time[lo] + (tile_time[hi] - tile_time[lo]) * ((float)r / (float)step) : tile_time[lo];
+        }
+        __syncthreads();
+    }
     float     sum = 0.0f;
     for (int64_t i = tid; i < n; i += 1024) sum += tile_time[i];
     for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
@@ -152,10 +163,10 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const float* tile_time
     }
 }
 
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
+hipError_t launch_tile_order(float* tile_time, int64_t n_tiles, float factor, int tiles_x, int step, int32_t* order,
                              hipStream_t stream)
 {
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_time, n_tiles, factor, tiles_x, order);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, tile_time, n_tiles, factor, tiles_x, step, order);
     return hipGetLastError();
 }
 

@@ -291,10 +291,10 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
                            draws_total);
                 continue;
             }
-        } else if (item >= args.num_tiles) {
+        } else if (item * (PROBE ? (int64_t)args.probe_step : 1) >= args.num_tiles) {
             break;
         }
-        const int64_t  slot    = args.order ? args.order[item] : item;
+        const int64_t  slot    = PROBE ? item * args.probe_step : (args.order ? args.order[item] : item);
         const uint64_t t_start = (PROBE || args.tile_diag) ? __builtin_amdgcn_s_memrealtime() : 0;
         const int32_t  tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
         const uint32_t px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
@@ -408,7 +408,7 @@ KernelFn probe_rrnee(int waves);
 KernelFn tail_direct(int variant, bool replay); // DirectLighting with tail chunks, 3 or 4 waves per SIMD
                                                  // (sp_mega_tail.hip; replay: an image light, 4 waves)
 KernelFn fused_chunks();           // the sample chunks' fused form, 4 waves per SIMD (sp_mega_tail.hip)
-hipError_t launch_tile_order(const float* tile_time, int64_t n_tiles, float factor, int tiles_x, int32_t* order,
+hipError_t launch_tile_order(float* tile_time, int64_t n_tiles, float factor, int tiles_x, int step, int32_t* order,
                              hipStream_t stream);
 
 } // namespace spd
