@@ -1489,10 +1489,12 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             pr.tile_time = s->d_tile_time;
             pr.counters  = s->probe_counters; // the probe's rays are not the render's
             pr.tile_diag = nullptr;
-            // every 2nd slot timed where tail chunks follow (the others interpolated by the order kernel:
-            // bunny +0.25 %, spheres +0.8 %, lucy +0.2 %); IterativeRRNEE, whose order has no tail
-            // chunks behind it, lost 2-4 % on elf's shard with it (profiles/r06/tail/ab_probe_step.log)
-            pr.probe_step = (integ == SP_INTEGRATOR_DIRECT_LIGHTING && (tail_auto || p->tail_fraction > 0.0f)) ? 2 : 1;
+            // every 2nd slot timed where tail chunks follow and a wave takes 6 tiles or more (the others
+            // interpolated by the order kernel: bunny +0.25 %, lucy +0.2 %); at 4 tiles per wave the
+            // 2-way shard lost 2.5 % with it (spheres gained 0.6-0.8 %), and IterativeRRNEE, whose order
+            // has no tail chunks behind it, lost 2-4 % on elf's shard (profiles/r06/tail/ab_probe_step*.log)
+            pr.probe_step = (integ == SP_INTEGRATOR_DIRECT_LIGHTING && (tail_auto || p->tail_fraction > 0.0f) &&
+                             n_tiles >= 6 * (int64_t)waves) ? 2 : 1;
             if (const char* v = std::getenv("SP_PROBE_STEP")) pr.probe_step = std::max(1, std::atoi(v));
             SP_HIP(spd::launch_probe(sc_run, pr, integ, variant, blocks, lds_bytes, stream));
             // cost estimates blended with their queue neighbours only where those sit at known
