@@ -530,19 +530,19 @@ def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
         # by ck_count and ck_shade, the 2-byte draw count, radiance written once and summed
         alg = st.rng_draws * MT_BYTES_PER_DRAW + samples * (16 * 3 + 2 * 2 + 12 * 2) + pixels * PIXEL_BYTES + scene_bytes
         achieved = alg / (kernel_ms * 1e-3) / 1e9
-        # fused form (3 launches): ck_camera, then the counts and the chunks in sp_tail_kernel, ck_sum
+        # fused form (3 launches): ck_camera, then the counts and the chunks in sp_fused_kernel, ck_sum
         fused = st.launches == 3
-        kernels = "ck_camera+sp_tail_kernel+ck_sum" if fused else "ck_camera+ck_count+ck_shade+ck_sum"
+        kernels = "ck_camera+sp_fused_kernel+ck_sum" if fused else "ck_camera+ck_count+ck_shade+ck_sum"
         if tj is not None:  # the frame's kernels together, like the time
             traffic = sum(v["hbm_bytes_per_launch"] for k, v in tj.get("kernels", {}).items()
-                          if k.startswith("ck_") or (fused and k == "sp_tail_kernel")) or traffic
+                          if k.startswith("ck_") or (fused and k == "sp_fused_kernel")) or traffic
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kernels,
                 "traffic_source": traffic_source(args, tj),
                 "scene_bytes": scene_bytes,
                 "kernel_ms": round(kernel_ms, 3), "alg_bytes_per_launch": alg,
                 # the shading kernel: most of the frame's time
-                "valu": valu_of(args, "sp_tail_kernel" if fused else "ck_shade")}
+                "valu": valu_of(args, "sp_fused_kernel" if fused else "ck_shade")}
     if st.pipeline == 1 or args.integrator != "direct_lighting":  # megakernel
         # stage_ms[0]: the render kernel alone, [1]: the tile-order probe + partition before it
         # (HIP events on the render stream; sp_render_stats)
