@@ -530,9 +530,11 @@ def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
         # by ck_count and ck_shade, the 2-byte draw count, radiance written once and summed
         alg = st.rng_draws * MT_BYTES_PER_DRAW + samples * (16 * 3 + 2 * 2 + 12 * 2) + pixels * PIXEL_BYTES + scene_bytes
         achieved = alg / (kernel_ms * 1e-3) / 1e9
-        # fused form (3 launches): ck_camera, then the counts and the chunks in sp_fused_kernel, ck_sum
-        fused = st.launches == 3
-        kernels = "ck_camera+sp_fused_kernel+ck_sum" if fused else "ck_camera+ck_count+ck_shade+ck_sum"
+        # fused form: (ck_camera, unless the camera pass runs in the fused queue: 2 launches), then the
+        # counts and the chunks in sp_fused_kernel, ck_sum
+        fused = st.launches <= 3
+        kernels = (("ck_camera+" if st.launches == 3 else "") + "sp_fused_kernel+ck_sum") if fused \
+            else "ck_camera+ck_count+ck_shade+ck_sum"
         if tj is not None:  # the frame's kernels together, like the time
             traffic = sum(v["hbm_bytes_per_launch"] for k, v in tj.get("kernels", {}).items()
                           if k.startswith("ck_") or (fused and k == "sp_fused_kernel")) or traffic

@@ -953,6 +953,12 @@ int sp_render_tiles(sp_scene* s, const sp_render_params* p, float* d_out, sp_ren
 #ifndef SP_CK_FUSED
 #define SP_CK_FUSED 1
 #endif
+#ifndef SP_CK_CAMFOLD
+#define SP_CK_CAMFOLD 1
+#endif
+#ifndef SP_CK_CAM_BLOCK
+#define SP_CK_CAM_BLOCK 32
+#endif
 #ifndef SP_CK_FRONT_DIV
 #define SP_CK_FRONT_DIV 8
 #endif
@@ -1331,7 +1337,7 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             if (lds_bytes + lds_static > 160 * 1024) fused = false;
         }
         if (fused) {
-            const size_t a_hdr = 256, need = a_hdr + ((size_t)n_tiles * 4 + 255) / 256 * 256;
+            const size_t a_hdr = 256, a_rdy = ((size_t)n_tiles * 4 + 255) / 256 * 256, need = a_hdr + 2 * a_rdy;
             if (need > s->tail_cap) {
                 if (s->tail_buf) (void)hipFree(s->tail_buf);
                 s->tail_buf = nullptr;
@@ -1353,8 +1359,19 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             ta.snap_ctl    = a.snap_ctl;
             ta.draws       = a.draws;
             ta.ready       = reinterpret_cast<uint32_t*>(tb + a_hdr);
+            // the camera pass as the queue's first items (SP_CK_CAMFOLD; blocks of SP_CK_CAM_BLOCK
+            // samples per item) instead of the ck_camera kernel before it
+            bool cam_fold = SP_CK_CAMFOLD;
+            if (const char* v = std::getenv("SP_CK_CAMFOLD")) cam_fold = std::atoi(v) != 0;
+            if (cam_fold) {
+                ta.cam_block = SP_CK_CAM_BLOCK;
+                if (const char* v = std::getenv("SP_CK_CAM_BLOCK")) ta.cam_block = (uint32_t)std::max(1, std::atoi(v));
+                ta.n_cam     = n_tiles * (int64_t)((spp_u + ta.cam_block - 1) / ta.cam_block);
+                ta.cam_done  = reinterpret_cast<uint32_t*>(tb + a_hdr + a_rdy);
+                ta.draws_out = a.draws;
+            }
             SP_HIP(hipMemcpyAsync(tb, &ta, sizeof(ta), hipMemcpyHostToDevice, stream));
-            SP_HIP(hipMemsetAsync(ta.ready, 0, (size_t)n_tiles * 4, stream));
+            SP_HIP(hipMemsetAsync(ta.ready, 0, 2 * a_rdy, stream));
             spd::RenderArgs ra{};
             ra.out          = d_out;
             ra.tile_ids     = d_ids;
@@ -1372,14 +1389,15 @@ static int render_tiles_impl(sp_scene* s, const sp_render_params* p, float* d_ou
             int64_t front = std::max<int64_t>(1, t_waves / SP_CK_FRONT_DIV);
             if (const char* v = std::getenv("SP_CK_FRONT_DIV")) front = std::max<int64_t>(1, t_waves / std::max(1, std::atoi(v)));
             ra.tail_front = front;
+            ra.tail_cam   = ta.n_cam;
             ra.tail       = reinterpret_cast<const spd::TailArgs*>(tb);
             const int t_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->n_cu * t_per_cu,
                                                                                (n_tiles * (cp.chunks + 1) + 3) / 4));
             SP_HIP(hipEventRecord(s->ev0, stream));
-            SP_HIP(spd::chunk_camera(s->dev, a, s->n_cu, stream));
+            if (!cam_fold) SP_HIP(spd::chunk_camera(s->dev, a, s->n_cu, stream));
             SP_HIP(spd::launch_tail(s->dev, ra, 0, t_blocks, lds_bytes, stream));
             SP_HIP(spd::chunk_sum(s->dev, a, stream));
-            launches = 3;
+            launches = cam_fold ? 2 : 3;
         } else {
             SP_HIP(hipEventRecord(s->ev0, stream));
             SP_HIP(spd::chunk_render(s->dev, a, blocks, s->n_cu, stream));

@@ -193,6 +193,13 @@ struct TailArgs {
     // (Light::sample's usability), so the prep item replays each sample's Light::sample draws on the
     // stream itself (sp_chunk.hip ck_count's replay), twisting the store generation by generation
     int32_t         replay;
+    // sp_fused_kernel with the camera pass in its queue (n_cam > 0): items [0, n_cam) trace the
+    // camera rays of samples [b cam_block, (b + 1) cam_block) of one slot, tile-major, and count them
+    // into cam_done[slot]; a slot's prep waits for spp.  n_cam 0: ck_camera ran before the kernel.
+    int64_t         n_cam;
+    uint32_t        cam_block;
+    uint32_t*       cam_done;  // [K], zeroed per render
+    uint16_t*       draws_out; // [spp][n_px] the camera items' draw counts (= draws)
 };
 
 struct RenderArgs {
@@ -218,6 +225,7 @@ struct RenderArgs {
     // P = tail_front -- the memory-bound preps run beside the compute-bound chunks, each P tiles
     // ahead of its own chunks
     int64_t         tail_front;
+    int64_t         tail_cam;   // sp_fused_kernel: camera items ahead of the preps (TailArgs::n_cam)
     const TailArgs* tail;
     int32_t         probe_step; // sp_probe_kernel: times every probe_step-th slot (the order kernel fills the rest)
 };

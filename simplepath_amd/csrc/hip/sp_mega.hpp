@@ -45,6 +45,50 @@ __device__ __forceinline__ Ray tail_camera_ray(const Scene& sc, uint32_t px, uin
     return ray;
 }
 
+// Camera item c of the fused queue (TailArgs::n_cam): samples [b cam_block, (b + 1) cam_block) of
+// list slot c / blocks -- sp_chunk.hip ck_camera's work for them (Integrator.cpp:277-283: intersect
+// lights, then geometry; the hit record, a light-only hit's radiance, the sample's draw count) --
+// then an agent-scope release and cam_done[slot] += samples done (the slot's prep waits for spp).
+__device__ __forceinline__ void fused_camera(const Scene& sc, const RenderArgs& args, const Rsq& q, Stack& st, int64_t c,
+                                             uint32_t lane, uint32_t dx, uint32_t dy)
+{
+    const TailArgs& ta     = *args.tail;
+    const int64_t   nb     = (args.spp + ta.cam_block - 1) / ta.cam_block;
+    const int64_t   slot   = c / nb;
+    const uint32_t  i0     = (uint32_t)(c % nb) * ta.cam_block;
+    const uint32_t  i1     = min(args.spp, i0 + ta.cam_block);
+    const int32_t   tile   = args.tile_ids ? args.tile_ids[slot] : (int32_t)slot;
+    const uint32_t  px     = (uint32_t)((tile % args.tiles_x) * 8) + dx;
+    const uint32_t  py     = (uint32_t)((tile / args.tiles_x) * 8) + dy;
+    const bool      inside = px < (uint32_t)sc.width && py < (uint32_t)sc.height;
+    const size_t    p      = (size_t)slot * 64 + lane;
+    for (uint32_t i = i0; i < i1; ++i) {
+        float4   rec   = make_float4(0.0f, __uint_as_float(0xffffffffu), 0.0f, 0.0f);
+        rgb      L     = mkc(0, 0, 0);
+        uint32_t ndraw = 0;
+        if (inside && sc.max_depth > 0) {
+            const Ray      ray = tail_camera_ray(sc, px, py, i, q);
+            const LightHit lh  = scene_intersect_lights(sc, ray, k_ray_epsilon, k_infinite, st);
+            const Hit      h   = scene_intersect(sc, ray, k_ray_epsilon, lh.hit ? lh.t : k_infinite, st);
+            if (h.code != 0xffffffffu) {
+                rec   = make_float4(h.t, __uint_as_float(h.code), h.beta, h.gamma);
+                ndraw = sample_draws(sc, finish_hit(sc, h, ray, q), neg(ray.d), q);
+            } else if (lh.hit) {
+                L = cadd(L, cmul(mkc(1, 1, 1), light_hit_L(sc, lh, ray.d, q)));
+            }
+        }
+        ta.draws_out[(size_t)i * ta.n_px + p]      = (uint16_t)ndraw;
+        ta.hits[(size_t)i * ta.n_px + p]           = rec;
+        ta.L[((size_t)i * 3 + 0) * ta.n_px + p] = L.r;
+        ta.L[((size_t)i * 3 + 1) * ta.n_px + p] = L.g;
+        ta.L[((size_t)i * 3 + 2) * ta.n_px + p] = L.b;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(ta.cam_done + slot, i1 - i0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Prep item k (queue item k < K): tile order[k]'s camera rays (Integrator.cpp:277-283: intersect
 // lights, then geometry) for every sample, their hit records and the radiance of light-only hits;
 // each sample's draw count (sample_draws) summed into the stream position at every chunk start;
@@ -76,6 +120,13 @@ __device__ __forceinline__ void tail_prep(const Scene& sc, const RenderArgs& arg
     if (inside) rng_seed_twisted(rng, ((px << 16u) | py) ^ 0xb0ae9d99u);
     uint32_t T = 0; // stream position (words drawn) before sample i
     if constexpr (DRAWS) {
+        if (ta.n_cam > 0) { // the camera items of this slot (all taken before any prep) have finished
+            if (lane == 0)
+                while (__hip_atomic_load(ta.cam_done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < args.spp)
+                    __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         // the sample-chunk pipeline's form: counts from ck_camera, summed in batches of loads that
         // are all in flight together (sp_chunk.hip ck_count)
         const uint16_t* dp = ta.draws + p;
@@ -261,13 +312,19 @@ __device__ __forceinline__ void render_tiles_body(const Scene& sc, const RenderA
         if (lane == 0) grabbed = atomicAdd(args.tile_counter, 1);
         const int64_t item = __shfl(grabbed, 0, 64);
         if constexpr (TAIL == 2) {
-            { // every tile cut: preps interleaved with the chunks
+            { // every tile cut: [camera items] then the preps interleaved with the chunks
+                const int64_t NC = args.tail_cam;
+                if (item < NC) {
+                    fused_camera(sc, args, q, st, item, (uint32_t)lane, dx, dy);
+                    continue;
+                }
+                const int64_t it = item - NC;
                 const int64_t K = args.tail_prep, C = args.tail_items / max<int64_t>(1, K), P = min(args.tail_front, K);
-                if (item >= K + args.tail_items) break;
-                int64_t   idx  = item;
-                bool      prep = item < P;
+                if (it >= K + args.tail_items) break;
+                int64_t   idx  = it;
+                bool      prep = it < P;
                 if (!prep) {
-                    const int64_t j = item - P, full = K - P; // groups 0 .. full - 1: C chunks + prep g + P
+                    const int64_t j = it - P, full = K - P; // groups 0 .. full - 1: C chunks + prep g + P
                     if (j < full * (C + 1)) {
                         const int64_t g = j / (C + 1), r = j % (C + 1);
                         prep            = r == C;

@@ -136,15 +136,15 @@ def test_sample_chunks_equal_megakernel(scene_dir, monkeypatch, scene, bvh, chun
     # ray / draw counts.  Chunk counts that do not divide spp (13) leave a short last chunk; "0" =
     # automatic (16 for this many tiles).  Draw counts come from the camera pass, or from the
     # Light::sample replay (image light, or SP_CHUNK_REPLAY=1).
-    # With known counts the fused form (SP_CK_FUSED, default) runs ck_camera, then the counts and the
-    # chunks in one queue of the tail kernel (sp_mega.hpp), then ck_sum: 3 launches.
+    # With known counts the fused form (SP_CK_FUSED, default) runs the camera pass, the counts and the
+    # chunks in one queue (sp_fused_kernel, sp_mega.hpp), then ck_sum: 2 launches.
     monkeypatch.setenv("SP_CHUNK_REPLAY", replay)
     monkeypatch.setenv("SP_CK_FUSED", fused)
     s = load(scene_dir, scene, 72, 40, bvh=bvh)
     m, mst = sp.render_tiles(s, "direct_lighting", 13, pipeline="megakernel")
     c, cst = sp.render_tiles(s, "direct_lighting", 13, pipeline="chunks", chunks_per_pixel=int(chunks))
     known = replay == "0" and scene != "material_spheres_ibl.sp"
-    assert cst.pipeline == 3 and cst.launches == (3 if fused == "1" and known else 4)
+    assert cst.pipeline == 3 and cst.launches == (2 if fused == "1" and known else 4)
     assert np.array_equal(m.view(np.uint32), c.view(np.uint32)), rel_l2(c, m)
     assert (mst.rays, mst.shadow_rays, mst.samples, mst.rng_draws) == \
         (cst.rays, cst.shadow_rays, cst.samples, cst.rng_draws)

@@ -123,8 +123,8 @@ def test_auto_takes_the_tail_on_a_two_way_shard(scene_dir):
     assert ost.pipeline == sp.PIPELINES["chunks"]  # tail off (or below 128 spp): the old rule
 
 
-@pytest.mark.parametrize("front_div", ["1", "64", "100000"])
-def test_fused_sample_chunks(scene_dir, monkeypatch, front_div):
+@pytest.mark.parametrize("front_div,cam_block", [("1", "32"), ("64", "5"), ("100000", "1000")])
+def test_fused_sample_chunks(scene_dir, monkeypatch, front_div, cam_block):
     # the sample-chunk pipeline's fused form: ck_camera, then every tile's prep (stream positions,
     # generations into the store) and its chunks in one queue, prep g + P dealt after tile g's chunks
     # (P = persistent waves / SP_CK_FRONT_DIV: all preps first, some ahead, one ahead); equal to the
@@ -133,8 +133,12 @@ def test_fused_sample_chunks(scene_dir, monkeypatch, front_div):
     ids = np.arange(0, sp.TileScheduler(W, H).get_num_tiles(), 2, dtype=np.int32)  # 2560 tiles
     ref, rst = sp.render_tiles(s, "direct_lighting", 6, ids, pipeline="megakernel", tile_order_factor=-1.0)
     monkeypatch.setenv("SP_CK_FRONT_DIV", front_div)
+    monkeypatch.setenv("SP_CK_CAM_BLOCK", cam_block)  # camera items of 32, 5 (ragged) or all samples
     img, st = sp.render_tiles(s, "direct_lighting", 6, ids, pipeline="chunks", chunks_per_pixel=3)
-    assert st.launches == 3 and counts(st) == counts(rst) and same_bits(img, ref)
+    assert st.launches == 2 and counts(st) == counts(rst) and same_bits(img, ref)  # the camera pass in the queue
+    monkeypatch.setenv("SP_CK_CAMFOLD", "0")
+    img, st = sp.render_tiles(s, "direct_lighting", 6, ids, pipeline="chunks", chunks_per_pixel=3)
+    assert st.launches == 3 and counts(st) == counts(rst) and same_bits(img, ref)  # ck_camera before the queue
     monkeypatch.setenv("SP_CK_FUSED", "0")
     four, fst = sp.render_tiles(s, "direct_lighting", 6, ids, pipeline="chunks", chunks_per_pixel=3)
     assert fst.launches == 4 and counts(fst) == counts(rst) and same_bits(four, ref)
