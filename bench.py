@@ -104,7 +104,10 @@ def parse():
     if a.sim_world > 1 and not -1 <= a.sim_rank < a.sim_world:
         ap.error("--sim-rank must be -1 or in [0, --sim-world)")
     # tools/gpu_pmc_*.sh output names (PMC passes profile rank 0's shard)
-    tag = a.scene + (f"_shard{a.sim_world}" if a.sim_world > 1 else "") + (f"_r{a.sim_rank}" if a.sim_world > 1 and a.sim_rank > 0 else "")
+    # the per-rank workload the counters must describe: a --sim-world shard, or with --gpus N rank 0's
+    # shard of N (the PMC passes profile `--sim-world N`, the same tiles and calls)
+    a.shard_n = a.sim_world if a.sim_world > 1 else (a.gpus if a.gpus > 1 else 0)
+    tag = a.scene + (f"_shard{a.shard_n}" if a.shard_n > 1 else "") + (f"_r{a.sim_rank}" if a.sim_world > 1 and a.sim_rank > 0 else "")
     a.traffic_json = a.traffic_json or os.path.join(ROOT, "profiles", f"pmc_bench_{tag}.json")
     a.valu_json = a.valu_json or os.path.join(ROOT, "profiles", f"pmc_valu_bench_{tag}.json")
     sc = SCENES[a.scene]
@@ -486,7 +489,7 @@ def valu_of(args, kernel):
     except (OSError, ValueError):
         return None
     if (vj.get("width"), vj.get("height"), vj.get("spp"), vj.get("scene", "bunny"), vj.get("sim_world", 0)) != \
-            (args.width, args.height, args.spp, args.scene, args.sim_world):
+            (args.width, args.height, args.spp, args.scene, args.shard_n):
         return None
     if not pmc_of_this_build(vj):
         return None
@@ -517,7 +520,7 @@ def roofline_of(stats, pixels, args, kernel_ms, scene_bytes=0):
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
             if (tj.get("width") == args.width and tj.get("height") == args.height and tj.get("spp") == args.spp
-                    and tj.get("scene", "bunny") == args.scene and tj.get("sim_world", 0) == args.sim_world
+                    and tj.get("scene", "bunny") == args.scene and tj.get("sim_world", 0) == args.shard_n
                     and pmc_of_this_build(tj)):
                 traffic = tj.get("hbm_bytes_per_launch")
             else:
