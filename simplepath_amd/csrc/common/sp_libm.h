@@ -364,6 +364,52 @@ SP_HD float lm_cosf(float y)
     return ((iy & 0x7fffffffu) > 0x7f800000u) ? x86_quiet(y) : x86_default_nan();
 }
 
+// sinf(y) and cosf(y) of one BOUNDED argument (|y| < 120, finite), each bit-identical to the calls
+// above: both take the same reduction and the same two polynomials, so one reduction and one of
+// each polynomial serve both -- where the separate calls each evaluate both polynomials whenever
+// the wave's lanes hold both quadrant parities.
+SP_HD void lm_sincosf_bounded(float y, float* s_out, float* c_out)
+{
+#if defined(SP_XP_FASTLIBM) && defined(__HIP_DEVICE_COMPILE__) // timing-only bound (sp_path.hpp SP_XP_*)
+    *s_out = __sinf(y); *c_out = __cosf(y); return;
+#endif
+    const uint32_t iy     = f2u(y);
+    const uint32_t abstop = (iy >> 20) & 0x7ffu;
+    double         x      = (double)y;
+    int            n      = 0;
+    int            tb     = 0;
+    if (abstop > 0x3f3u) {
+        const double r  = x * sc(SC_HPI_INV);
+        n               = (((int32_t)r) + 0x800000) >> 24;
+        x               = dfma(-(double)n, sc(SC_HPI), x);
+        x               = x * sincos_sign(n & 3); // x2 below is the square of the signed x: exact
+        tb              = (n & 2) ? 1 : 0;
+    }
+    const double x2 = x * x;
+    const double s1 = dfma(x2, sc(SC_S3), vk<glibc::SINCOSF_T[SC_S2]>(x2));
+    const double x3 = x2 * x;
+    const double x7 = x2 * x3;
+    const float  ps = (float)dfma(s1, x7, dfma(x3, sc(SC_S1), x));
+    const double x4 = x2 * x2;
+    const double c1 = dfma(x2, sc(SC_C1), vk<glibc::SINCOSF_T[SC_C0]>(x2));
+    const double c2 = dfma(x2, sc(SC_C4), vk<glibc::SINCOSF_T[SC_C3]>(x2));
+    const double x6 = x2 * x4;
+    const float  pr = (float)dfma(c2, x6, dfma(x4, sc(SC_C2), c1));
+    const float  pc = tb ? -pr : pr;
+    const bool   odd = (n & 1) != 0;
+    *s_out = odd ? pc : ps;
+    *c_out = odd ? ps : pc;
+    if (abstop <= 0x397u) { *s_out = y; *c_out = 1.0f; }
+}
+
+// sinf(y) and cosf(y) of any argument: the fused form where it applies, the two calls elsewhere
+SP_HD void lm_sincosf(float y, float* s_out, float* c_out)
+{
+    if (((f2u(y) >> 20) & 0x7ffu) <= 0x42eu) { lm_sincosf_bounded(y, s_out, c_out); return; }
+    *s_out = lm_sinf(y);
+    *c_out = lm_cosf(y);
+}
+
 // ------------------------------------------------------------------------------------ erff
 SP_HD float lm_erff(float x)
 {

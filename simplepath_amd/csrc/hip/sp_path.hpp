@@ -1628,10 +1628,9 @@ __device__ __forceinline__ EnvSample env_sample(const EnvMap& e, P2 u)
     }
     const float theta     = d1 * k_pi;
     const float phi       = d0 * 2.0f * k_pi;
-    const float cos_theta = lm_cosf(theta);
-    const float sin_theta = lm_sinf(theta);
-    const float sin_phi   = lm_sinf(phi);
-    const float cos_phi   = lm_cosf(phi);
+    float       sin_theta, cos_theta, sin_phi, cos_phi;
+    lm_sincosf(theta, &sin_theta, &cos_theta);
+    lm_sincosf(phi, &sin_phi, &cos_phi);
     s.wi  = xfm_vector(e.l2w, mk(sin_theta * cos_phi, cos_theta, sin_theta * sin_phi));
     s.pdf = (sin_theta == 0.0f) ? 0.0f : map_pdf / (2.0f * (k_pi * k_pi) * sin_theta);
     s.L   = env_texel(e, d0, d1);
@@ -1800,7 +1799,9 @@ __device__ __forceinline__ f3 sample_uniform_sphere(P2 u)
     const float z   = 1.0f - 2.0f * u.x;
     const float r   = sqrt_unit(std_max(0.0f, 1.0f - z * z));
     const float phi = (float)(2.0 * (double)k_pi * (double)u.y);
-    return mk(r * lm_cosf<true>(phi), r * lm_sinf<true>(phi), z); // u in [0, 1): |phi| < 2 pi
+    float       sp, cp;
+    lm_sincosf_bounded(phi, &sp, &cp); // u in [0, 1): |phi| < 2 pi
+    return mk(r * cp, r * sp, z);
 }
 // math/Sampling.h:235
 __device__ __forceinline__ f3 sample_uniform_hemisphere(P2 u)
@@ -1808,7 +1809,9 @@ __device__ __forceinline__ f3 sample_uniform_hemisphere(P2 u)
     const float y   = u.x;
     const float r   = sqrt_unit(std_max(0.0f, 1.0f - y * y));
     const float phi = 2.0f * k_pi * u.y;
-    return mk(r * lm_cosf<true>(phi), y, r * lm_sinf<true>(phi)); // u in [0, 1): |phi| < 2 pi
+    float       sp, cp;
+    lm_sincosf_bounded(phi, &sp, &cp); // u in [0, 1): |phi| < 2 pi
+    return mk(r * cp, y, r * sp);
 }
 // math/Sampling.cpp:304
 __device__ __forceinline__ P2 concentric_disk(P2 u)
@@ -1822,8 +1825,10 @@ __device__ __forceinline__ P2 concentric_disk(P2 u)
     float theta, rad;
     if (abs_f(ox) > abs_f(oy)) { rad = ox; theta = pi_over_4 * (oy / ox); }
     else { rad = oy; theta = pi_over_2 - pi_over_4 * (ox / oy); }
-    r.x = rad * lm_cosf<true>(theta); // |theta| <= 3 pi / 4
-    r.y = rad * lm_sinf<true>(theta);
+    float st, ct;
+    lm_sincosf_bounded(theta, &st, &ct); // |theta| <= 3 pi / 4
+    r.x = rad * ct;
+    r.y = rad * st;
     return r;
 }
 __device__ __forceinline__ f3 sample_cosine_hemisphere(P2 u)
@@ -1935,8 +1940,8 @@ __device__ __forceinline__ P2 beckmann_sample11(float cos_theta_i, float U1, flo
     P2 s;
     if (cos_theta_i > .9999f) {
         const float r  = sqrt_f(-lm_logf(1.0f - U1));
-        const float sp = lm_sinf<true>(2.0f * k_pi * U2); // U2 in [0, 1): bounded argument
-        const float cp = lm_cosf<true>(2.0f * k_pi * U2);
+        float       sp, cp;
+        lm_sincosf_bounded(2.0f * k_pi * U2, &sp, &cp); // U2 in [0, 1): bounded argument
         s.x = r * cp;
         s.y = r * sp;
         return s;
@@ -2100,8 +2105,8 @@ __device__ __forceinline__ P2 beckmann_sample11_pre(const BeckPre& p, float U1, 
     P2 s;
     if (p.steep) {
         const float r  = sqrt_f(-lm_logf(1.0f - U1));
-        const float sp = lm_sinf<true>(2.0f * k_pi * U2); // U2 in [0, 1): bounded argument
-        const float cp = lm_cosf<true>(2.0f * k_pi * U2);
+        float       sp, cp;
+        lm_sincosf_bounded(2.0f * k_pi * U2, &sp, &cp); // U2 in [0, 1): bounded argument
         s.x = r * cp;
         s.y = r * sp;
         return s;

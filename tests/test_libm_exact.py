@@ -20,7 +20,7 @@ def checker(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("fn", ["expf", "logf", "sinf", "cosf", "erff", "acosf", "atanf", "fmod1", "roundf", "powf", "atan2f"])
+@pytest.mark.parametrize("fn", ["expf", "logf", "sinf", "cosf", "sincosf", "erff", "acosf", "atanf", "fmod1", "roundf", "powf", "atan2f"])
 def test_libm_matches_glibc(checker, fn):
     out = subprocess.run([checker, fn, "4099", "4"], capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stdout
@@ -32,5 +32,5 @@ def test_full_sweep_log():
     if not os.path.exists(log):
         pytest.skip("full 2^32 sweep log not recorded yet")
     text = open(log).read()
-    for fn in ["expf", "logf", "sinf", "cosf", "erff", "acosf", "atanf", "fmod1", "roundf"]:
+    for fn in ["expf", "logf", "sinf", "cosf", "sincosf", "erff", "acosf", "atanf", "fmod1", "roundf"]:
         assert f"{fn} checked=4294967296 mismatches=0" in text

@@ -1,6 +1,6 @@
 // Exhaustive bit-exactness check of spm::lm_* (simplepath_amd/csrc/common/sp_libm.h) against the
 // host glibc float libm.  Usage: libm_exhaustive <func> [stride] [threads]
-//   func: sinf cosf expf logf erff acosf atanf fmod1 roundf powf atan2f
+//   func: sinf cosf sincosf expf logf erff acosf atanf fmod1 roundf powf atan2f
 // Prints "<func> checked=<n> mismatches=<m>" and up to 8 examples.
 #include "../simplepath_amd/csrc/common/sp_libm.h"
 #include <atomic>
@@ -76,6 +76,25 @@ int main(int argc, char** argv)
                     const float want = powf(x, y), got = spm::lm_powf(x, y);
                     ++c;
                     if (bits(want) != bits(got)) { ++b; report(x, y, got, want); }
+                }
+                checked += c;
+                bad += b;
+            });
+        for (auto& x : th) x.join();
+    } else if (fn == "sincosf") {  // the fused forms: bounded where abstop <= 0x42e (|x| < 120), general elsewhere
+        std::vector<std::thread> th;
+        const uint64_t total = 1ull << 32;
+        for (int t = 0; t < nth; ++t)
+            th.emplace_back([&, t] {
+                uint64_t c = 0, b = 0;
+                for (uint64_t u = (uint64_t)t * stride; u < total; u += (uint64_t)nth * stride) {
+                    const float x = flt((uint32_t)u);
+                    float s, co;
+                    if ((((uint32_t)u >> 20) & 0x7ffu) <= 0x42eu) spm::lm_sincosf_bounded(x, &s, &co);
+                    else spm::lm_sincosf(x, &s, &co); // the general form's fallback
+                    ++c;
+                    if (bits(s) != bits(sinf(x))) { ++b; report(x, 0.0f, s, sinf(x)); }
+                    if (bits(co) != bits(cosf(x))) { ++b; report(x, 1.0f, co, cosf(x)); }
                 }
                 checked += c;
                 bad += b;
