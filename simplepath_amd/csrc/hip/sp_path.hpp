@@ -2166,15 +2166,25 @@ __device__ __forceinline__ MSample mf_sample_pre(const Material& m, const BeckPr
     rng_raw2<NT, PAIR>(rng, u2, u1); // U2 first, then U1
     return mf_sample_pre_u(m, p, wo, u2, u1, q);
 }
-// mf_sample_pre from its two drawn (tempered) words
-__device__ __forceinline__ MSample mf_sample_pre_u(const Material& m, const BeckPre& p, f3 wo, uint64_t u2, uint64_t u1,
-                                                   const Rsq& q)
+// mf_sample_pre_u's scalars: the sampled direction and pdf and the eval's factors, the microfacet
+// colour left out (color = ((R * D) * G) * F / den per channel, 0 when black)
+struct MGeom {
+    f3    dir;
+    float pdf; // 0: no sample (mf_sample_pre_u returns black, pdf 0)
+    float D, G, F, den;
+    bool  valid; // false: mf_sample_pre_u's early returns (black, no direction, pdf 0, no props)
+    bool  black;
+};
+__device__ __forceinline__ MGeom mf_sample_geom(const Material& m, const BeckPre& p, f3 wo, uint64_t u2, uint64_t u1,
+                                                const Rsq& q)
 {
-    MSample r;
-    r.color = mkc(0, 0, 0);
-    r.dir   = mk(0, 0, 0);
-    r.pdf   = 0.0f;
-    r.props = 0;
+    MGeom g;
+    g.dir   = mk(0, 0, 0);
+    g.pdf   = 0.0f;
+    g.D = g.G = g.F = 0.0f;
+    g.den   = 1.0f;
+    g.valid = false;
+    g.black = true;
     const float U2 = canonical_from_u64(u2);
     const float U1 = canonical_from_u64(u1);
     P2          sl = beckmann_sample11_pre(p, U1, U2);
@@ -2186,33 +2196,57 @@ __device__ __forceinline__ MSample mf_sample_pre_u(const Material& m, const Beck
     f3 wh = normalize(mk(-sl.x, 1.0f, -sl.y), q);
     if (p.flip) wh = neg(wh);
     const float dp = dot(wo, wh);
-    if (dp < 0.0f) return r;
+    if (dp < 0.0f) return g;
     const f3 wi = add(neg(wo), scale(2.0f * dot(wo, wh), wh));
-    if (!same_hemisphere(wo, wi)) return r;
+    if (!same_hemisphere(wo, wi)) return g;
     // beck_pdf(m, wo, wh) with G1(wo) = 1 / (1 + lambda(wo))
     const float bpdf = m.sample_visible_area ? beck_D(m, wh) * (1.0f / (1.0f + p.lam_wo)) * abs_f(dot(wo, wh)) / abs_f(wo.y)
                                              : beck_D(m, wh) * abs_f(wh.y);
-    r.pdf = bpdf / (4.0f * dp);
+    g.pdf   = bpdf / (4.0f * dp);
+    g.dir   = wi;
+    g.valid = true;
     // mf_eval(m, wo, wi) with G = 1 / (1 + lambda(wo) + lambda(wi))
-    {
-        const float ao = abs_f(wo.y), ai = abs_f(wi.y);
-        if (ai == 0.0f || ao == 0.0f) {
-            r.color = mkc(0, 0, 0);
-        } else {
-            f3 h = add(wi, wo);
-            if (h.x == 0.0f && h.y == 0.0f && h.z == 0.0f) {
-                r.color = mkc(0, 0, 0);
-            } else {
-                h             = normalize(h, q);
-                const float f = fresnel_dielectric(dot(wi, h), 1.0f, m.microfacet_ior);
-                const float G = 1.0f / (1.0f + p.lam_wo + beck_lambda(m, wi));
-                r.color = cdivs(cscale(cscale(cscale(m.microfacet_r, beck_D(m, h)), G), f), 4.0f * ai * ao);
-            }
-        }
-    }
-    r.dir   = wi;
+    const float ao = abs_f(wo.y), ai = abs_f(wi.y);
+    if (ai == 0.0f || ao == 0.0f) return g;
+    f3 h = add(wi, wo);
+    if (h.x == 0.0f && h.y == 0.0f && h.z == 0.0f) return g;
+    h       = normalize(h, q);
+    g.F     = fresnel_dielectric(dot(wi, h), 1.0f, m.microfacet_ior);
+    g.G     = 1.0f / (1.0f + p.lam_wo + beck_lambda(m, wi));
+    g.D     = beck_D(m, h);
+    g.den   = 4.0f * ai * ao;
+    g.black = false;
+    return g;
+}
+// one channel of the sample's colour: cdivs(cscale(cscale(cscale(R, D), G), F), den) per channel
+__device__ __forceinline__ float mf_geom_channel(const MGeom& g, float R) { return g.black ? 0.0f : (((R * g.D) * g.G) * g.F) / g.den; }
+// mf_sample_pre from its two drawn (tempered) words
+__device__ __forceinline__ MSample mf_sample_pre_u(const Material& m, const BeckPre& p, f3 wo, uint64_t u2, uint64_t u1,
+                                                   const Rsq& q)
+{
+    const MGeom g = mf_sample_geom(m, p, wo, u2, u1, q);
+    MSample     r;
+    r.color = mkc(0, 0, 0);
+    r.dir   = g.dir;
+    r.pdf   = g.pdf;
+    r.props = 0;
+    if (!g.valid) return r;
+    r.color = mkc(mf_geom_channel(g, m.microfacet_r.r), mf_geom_channel(g, m.microfacet_r.g), mf_geom_channel(g, m.microfacet_r.b));
     r.props = PROP_GLOSSY | PROP_REFLECTIVE;
     return r;
+}
+// The rho estimate's sum over one sample: r += color * |wi.y| / pdf per channel.  A grey microfacet
+// colour (the three channels' bits equal: every glossy material a scene file makes has R = 1)
+// computes one channel -- the other two would repeat its operations on the same bits.
+__device__ __forceinline__ void rho_accumulate(rgb& r, const MGeom& g, rgb R, bool grey)
+{
+    if (!(g.pdf > 0.0f)) return;
+    const float ay = abs_f(g.dir.y);
+    r.r = r.r + (mf_geom_channel(g, R.r) * ay) / g.pdf;
+    if (!grey) {
+        r.g = r.g + (mf_geom_channel(g, R.g) * ay) / g.pdf;
+        r.b = r.b + (mf_geom_channel(g, R.b) * ay) / g.pdf;
+    }
 }
 // SP_RHO_ALIGNED: the estimate's 32 words (idx .. idx + 31, reserved: no twist) are read as one
 // aligned 16-byte pair per sample, whatever the parity of idx: at an odd idx a sample's two words
@@ -2223,11 +2257,15 @@ __device__ __forceinline__ MSample mf_sample_pre_u(const Material& m, const Beck
 #ifndef SP_RHO_ALIGNED
 #define SP_RHO_ALIGNED 0
 #endif
+#ifndef SP_RHO_GREY // one channel of the rho estimate for a grey microfacet colour (rho_accumulate)
+#define SP_RHO_GREY 1
+#endif
 template <bool PAIR = (SP_RNG_PAIR != 0), bool ALIGN = (SP_RHO_ALIGNED != 0), bool TOUCH = (SP_RHO_TOUCH != 0)>
 __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, const Rsq& q)
 {
     const BeckPre p = beck_pre(m, wo, q);
     rgb           r = mkc(0, 0, 0);
+    const bool grey = SP_RHO_GREY && f2u(m.microfacet_r.r) == f2u(m.microfacet_r.g) && f2u(m.microfacet_r.r) == f2u(m.microfacet_r.b);
     rng_reserve(rng, 32); // the loop below draws at most 32 words and never twists
 #if SP_RHO_TOUCH
     if constexpr (TOUCH) rng_touch(rng, 32, (__attribute__((address_space(3))) void*)rho_rng_sink);
@@ -2245,16 +2283,19 @@ __device__ __forceinline__ rgb mf_rho16(const Material& m, f3 wo, Rng& rng, cons
             const ulonglong2 w  = *reinterpret_cast<const ulonglong2*>(b);
             const uint64_t   w0 = odd ? carry : w.x, w1 = odd ? w.x : w.y;
             carry               = w.y;
-            const MSample s     = mf_sample_pre_u(m, p, wo, mt_temper(w0), mt_temper(w1), q);
-            if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
+            rho_accumulate(r, mf_sample_geom(m, p, wo, mt_temper(w0), mt_temper(w1), q), m.microfacet_r, grey);
         }
         rng_skip_reserved(rng, 32);
+        if (grey) r.g = r.b = r.r;
         return cdivs(r, (float)16u);
     }
     for (unsigned i = 0; i < 16u; ++i) {
-        const MSample s = mf_sample_pre<true, PAIR>(m, p, wo, rng, q);
-        if (s.pdf > 0.0f) r = cadd(r, cdivs(cscale(s.color, abs_f(s.dir.y)), s.pdf));
+        if (wo.y == 0.0f) continue; // mf_sample_pre: draws nothing, black
+        uint64_t u2, u1;
+        rng_raw2<true, PAIR>(rng, u2, u1); // U2 first, then U1
+        rho_accumulate(r, mf_sample_geom(m, p, wo, u2, u1, q), m.microfacet_r, grey);
     }
+    if (grey) r.g = r.b = r.r;
     return cdivs(r, (float)16u);
 }
 

@@ -107,3 +107,23 @@ def test_long_sample_chain(scene_dir):
             draws.add(gst.rng_draws)
             assert gst.rays == cst["rays"] and same_bits(g, c), (integrator, pipeline)
         assert len(draws) == 1 and draws.pop() > 64 * 312, integrator  # more than one generation per pixel
+
+
+@pytest.mark.parametrize("pipeline", ["megakernel", "chunks"])
+def test_coloured_microfacet_reflectance(scene_dir, pipeline):
+    # every glossy material a scene file makes has a white microfacet colour, and the rho estimate
+    # computes one channel for a grey one (sp_path.hpp rho_accumulate); a host-built scene may give
+    # any colour: here one glossy material coloured and the others grey, so waves hold both kinds
+    a = sp.Scene.from_file(os.path.join(scene_dir, "bunny.sp"))
+    a.set_resolution(40, 24)
+    d = a.desc()
+    glossy = [k for k in range(d.info.num_materials) if d.materials[k].kind == 1]
+    assert len(glossy) >= 2
+    for k in glossy[:: 2]:
+        d.materials[k].microfacet_r[0], d.materials[k].microfacet_r[1], d.materials[k].microfacet_r[2] = 0.9, 0.5, 0.2
+    s = sp.Scene.from_desc(d)
+    s.upload(device=0, bvh_mode=1)
+    for integrator in ["direct_lighting", "iterative_rrnee"]:
+        g, gst = sp.render_tiles(s, integrator, 3, pipeline=pipeline)
+        c, cst = oracle(s, integrator, 3)
+        assert gst.rays == cst["rays"] and same_bits(g, c), integrator
